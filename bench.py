@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the MI355X path-tracing megakernel on BASELINE.json's
+headline workload (config 2: book-cover scene, seed 2, 1280x720, r=64, d=50).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c5]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A step = one full frame rendered through the C-ABI (tray_render_async) with the
+scene already resident in HBM; for N > 1 the frame is split into interleaved
+8-row tiles (one shard per rank, no collective inside the render) and the step
+ends with ONE RCCL gather of the row tiles to rank 0 ("scaling": "strong": the
+frame is fixed as N grows). value = W*H*r*steps / max-over-ranks wall time.
+
+Also reported (rank 0):
+  roofline     the megakernel against the FP64 VALU roof (it is compute bound;
+               HBM traffic is ~1e-5 of the roof and reported under "hbm"):
+               achieved = algorithmic FP64 ops per launch / mean kernel time,
+               ops = 17*N_spheres*segments + 60*segments + 40*samples
+               (SURVEY.md §8(d)); segments are counted by the kernel itself in
+               an untimed launch (bit-exact with the oracle, tests/).
+  cpu_baseline the oracle (C port of the reference's CPU loop with the
+               reference's chunk-queue scheduler, ray/tracer.go:86-116) timed on
+               a bounded row sample of the same frame on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/sec, seed-2 book-cover scene 1280x720 r=64 d=50; per-pixel L∞ vs ref"
+
+CONFIGS = {
+    # name: (label, seed, half_extent, W, H, spp, depth)
+    "c1": ("C1 book-cover seed 2 400x225 r=16 d=12", 2, 11, 400, 225, 16, 12),
+    "c2": ("C2 book-cover seed 2 1280x720 r=64 d=50", 2, 11, 1280, 720, 64, 50),
+    "c3": ("C3 book-cover seed 2 3840x2160 r=256 d=50", 2, 11, 3840, 2160, 256, 50),
+    "c5": ("C5 dense RichScene(half-extent 22) seed 7 1920x1080 r=256 d=50", 7, 22, 1920, 1080, 256, 50),
+}
+
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector, AMD spec, FMA counted as 2 flops
+FP64_PEAK_OPS = FP64_PEAK_TFLOPS / 2  # T non-FMA FP64 ops/s (parity forbids contraction): 39.3
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--tile-rows", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-row-step", type=int, default=12, help="oracle renders every k-th row of the frame")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from tray_amd import _lib, ray, shard
+
+    label, seed, half, W, H, spp, depth = CONFIGS[args.config]
+    spheres = ray.rich_scene_array(seed, half)
+    cam = ray.RichSceneCamera()
+    cam.Initialize(W, H)
+    bg = ray._background(ray.DefaultBackground())
+    scene = _lib.DeviceScene(spheres, bg, local_rank)
+    params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
+    params = shard.shard_params(params, args.tile_rows, world, rank)
+    rows = _lib.params_rows(params)
+    out = torch.empty((rows, W, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def render(seg_ptr=None):
+        scene.render_async(cam._state, params, out.data_ptr(), seg_ptr, stream.cuda_stream)
+
+    def step():
+        render()
+        if world > 1:
+            shard.gather_image(out, H, args.tile_rows, world, rank)
+
+    # Untimed: per-pixel Scene.Hit counts for the roofline's algorithmic op count.
+    seg = torch.zeros((rows, W), dtype=torch.int32, device="cuda")
+    render(seg.data_ptr())
+    torch.cuda.synchronize()
+    segments_local = int(seg.to(torch.int64).sum().item())
+    del seg
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        render()
+        ev[i][1].record(stream)
+        if world > 1:
+            shard.gather_image(out, H, args.tile_rows, world, rank)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples = W * H * spp
+    value = samples * args.steps / elapsed / 1e6
+    rec = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: RichScene book-cover generator on the counter RNG (include/tray.h), RichSceneCamera",
+        "config": {
+            "workload": label,
+            "width": W, "height": H, "rays_per_pixel": spp, "max_depth": depth, "scene_seed": seed,
+            "spheres": int(len(spheres)), "output": "float3 f32 linear", "parallelism": f"row-tiles x{world}",
+            "tile_rows": args.tile_rows if world > 1 else 0,
+        },
+    }
+    if rank == 0:
+        local_samples = rows * W * spp
+        ops = 17.0 * len(spheres) * segments_local + 60.0 * segments_local + 40.0 * local_samples
+        achieved = ops / (kernel_ms * 1e-3) / 1e12
+        out_bytes = rows * W * 12 + len(spheres) * (32 + 48)
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(pmc_path):
+            try:
+                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        rec["roofline"] = {
+            "bound": "valu_fp64",
+            "achieved": round(achieved, 3),
+            "peak": FP64_PEAK_OPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP64_PEAK_OPS, 4),
+            "traffic": traffic,
+            "kernel_ms": round(kernel_ms, 4),
+            "segments_per_launch": segments_local,
+            "ops_per_launch": ops,
+            "ops_model": "17*N*segments + 60*segments + 40*samples, no FMA (SURVEY.md 8d)",
+            "hbm": {"achieved_GBs": round(out_bytes / (kernel_ms * 1e-3) / 1e9, 3), "peak_GBs": HBM_PEAK_GBS,
+                    "algorithmic_bytes_per_launch": out_bytes, "note": "not the bound"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed,
+                                               args.cpu_row_step)
+    print(json.dumps(rec), flush=True)
+    scene.release()
+    if dist:
+        dist.destroy_process_group()
+    return 0
+
+
+def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step):
+    """Oracle (C FP64 port of the reference CPU path, chunk-queue scheduler of
+    ray/tracer.go:86-116) on every `row_step`-th row of the same frame."""
+    from oracle import oracle as O
+
+    cores = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+    rows = np.arange(0, H, row_step, dtype=np.int32)
+    bg = np.array([1.0, 1.0, 1.0, 0.4, 0.65, 1.0])
+    t0 = time.perf_counter()
+    O.render_rows(spheres, bg, camera, W, H, spp, depth, 0.5, seed, rows, workers=cores, segments=False)
+    dt = time.perf_counter() - t0
+    samples = len(rows) * W * spp
+    return {"value": round(samples / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "seconds": round(dt, 3),
+            "sample": f"every {row_step}th row of the same frame ({len(rows)} rows x {W} px x r={spp}), "
+                      f"oracle/tray_oracle.c, {cores} pthreads"}
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,200 @@
+/*
+ * tray.h — C-ABI of the MI355X-native renderer for fortio/tray's per-pixel
+ * path-tracing loop.
+ *
+ * Drop-in seam: the Go API `(*ray.Tracer).Render(scene *ray.Scene) *image.RGBA`
+ * (ray/tracer.go:48) and `(*ray.Tracer).RenderLines(idx, yStart, yEnd, scene)`
+ * (ray/tracer.go:120). The reference has no FFI of its own (pure Go, no cgo), so
+ * each entry point below names the Go function/method whose work it replaces and
+ * INTEGRATION.md shows the cgo stub a maintainer would add to `ray/`.
+ *
+ * Rules (cgo-clean):
+ *   - plain C types only; no C++ exceptions cross this boundary;
+ *   - every caller buffer is caller-owned and is never retained after return;
+ *   - device-side state (uploaded scenes) is library-owned, released by
+ *     tray_scene_release()/tray_shutdown();
+ *   - every function returns TRAY_OK (0) or a negative tray_status; the message
+ *     of the last failure on the calling thread is tray_last_error().
+ *
+ * Arithmetic contract: all geometry and shading is IEEE FP64 evaluated in the
+ * reference's op order with no FMA contraction (ray/vec3.go, ray/objects.go,
+ * ray/materials.go, ray/camera.go). Division and sqrt are correctly rounded.
+ *
+ * Counter RNG contract (replaces fortio.org/rand v1.1.0, go.mod:9, which is not
+ * vendored): every random draw is one Philox4x32-10 block (Salmon et al. 2011,
+ * Random123 constants) with
+ *     key = (seed & 0xffffffff, seed >> 32)
+ *     ctr = (pixel, sample, bounce, (purpose << 24) | attempt)
+ *     pixel = y * width + x in GLOBAL image coordinates (tiling-independent)
+ *     purpose: 1 = anti-aliasing disc (ray/tracer.go:138), bounce = 0
+ *              2 = lens disc (ray/camera.go:128), bounce = 0
+ *              3 = scatter draw at hit number `bounce` (ray/materials.go:14,31,57)
+ *              4 = host scene generation, ctr = (draw_index, 0, 0, 4 << 24)
+ *     u0 = ((x1 << 32 | x0) >> 11) * 2^-53,  u1 = ((x3 << 32 | x2) >> 11) * 2^-53
+ * InDisc(r): attempt a = 0..31: x = 2u0-1, y = 2u1-1; accept x*x+y*y < 1 -> (x*r, y*r);
+ *            fallback (0,0).
+ * UnitVector: attempt a = 0..31 (Marsaglia 1972): x1 = 2u0-1, x2 = 2u1-1,
+ *            s = x1*x1+x2*x2; accept 0 < s < 1 -> f = 2*sqrt(1-s), (x1*f, x2*f, 1-2*s);
+ *            fallback (0,0,1).
+ * Float64 (Dielectric): u0 of attempt 0.
+ * A given (seed, pixel, sample) therefore renders the same colour for any
+ * tiling, row range, device count or launch geometry.
+ */
+#ifndef TRAY_H
+#define TRAY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRAY_ABI_VERSION 1
+
+typedef enum tray_status {
+    TRAY_OK = 0,
+    TRAY_ERR_INVALID_ARGUMENT = -1, /* bad sizes, null pointers, row range outside the image */
+    TRAY_ERR_UNSUPPORTED = -2,      /* object/material kind not representable (ray/objects.go:28-30) */
+    TRAY_ERR_DEVICE = -3,           /* HIP runtime failure */
+    TRAY_ERR_NO_DEVICE = -4,        /* no gfx950 device visible */
+    TRAY_ERR_TOO_LARGE = -5         /* scene or image exceeds a device limit */
+} tray_status;
+
+/* Material kinds: ray/materials.go:9 Lambertian, :23 Metal, :40 Dielectric. */
+typedef enum tray_material {
+    TRAY_LAMBERTIAN = 1,
+    TRAY_METAL = 2,
+    TRAY_DIELECTRIC = 3
+} tray_material;
+
+/* One *ray.Sphere with its Material (ray/objects.go:75-79). 72 bytes. */
+typedef struct tray_sphere {
+    double center[3];
+    double radius;
+    double albedo[3]; /* Lambertian.Albedo / Metal.Albedo; ignored for Dielectric */
+    double param;     /* Metal.Fuzz / Dielectric.RefIdx; ignored for Lambertian */
+    int32_t material; /* tray_material */
+    int32_t reserved; /* must be 0 */
+} tray_sphere;
+
+/* ray.AmbientLight (ray/objects.go:64-66): ColorA at the nadir blend end, ColorB at the zenith. */
+typedef struct tray_background {
+    double color_a[3];
+    double color_b[3];
+} tray_background;
+
+/* Public fields of ray.Camera (ray/camera.go:9-33). */
+typedef struct tray_camera_setup {
+    double position[3];
+    double look_at[3];
+    double up[3];
+    double vertical_fov;
+    double focal_length;
+    double focus_distance;
+    double aperture;
+} tray_camera_setup;
+
+/* Camera state after Camera.Initialize (ray/camera.go:34-39 computed fields). */
+typedef struct tray_camera {
+    double position[3];
+    double pixel00[3];
+    double pixel_x[3]; /* pixelXVector */
+    double pixel_y[3]; /* pixelYVector */
+    double defocus_u[3];
+    double defocus_v[3];
+    double aperture;
+    double focus_distance;
+    double focal_length;
+} tray_camera;
+
+/* Output pixel formats. */
+typedef enum tray_output {
+    TRAY_OUT_RGB_F64 = 0, /* linear mean colour, 3 x double per pixel (parity format) */
+    TRAY_OUT_RGB_F32 = 1, /* linear mean colour rounded to float, 3 x float per pixel */
+    TRAY_OUT_RGBA8 = 2    /* ColorF.ToSRGBA (ray/vec3.go:173-180) fused on device, A = 255 */
+} tray_output;
+
+/* Tracer fields (ray/tracer.go:25-36) after Render's defaulting (:64-79), plus
+ * the set of image rows this call renders.
+ *
+ * Row set: rows y in [y_start, y_end). With tile_rows > 0 the set is further
+ * restricted to row tiles owned by this shard: y is rendered iff
+ * ((y - y_start) / tile_rows) % tile_count == tile_index (interleaved row tiles
+ * for multi-GPU sharding). Output rows are COMPACT: the i-th rendered row is
+ * written at row i of the output buffer (row pitch = width pixels). */
+typedef struct tray_params {
+    int32_t width;
+    int32_t height;
+    int32_t max_depth;      /* Tracer.MaxDepth, > 0 */
+    int32_t rays_per_pixel; /* Tracer.NumRaysPerPixel, > 0 */
+    double ray_radius;      /* Tracer.RayRadius (AA disc radius in pixels) */
+    uint64_t seed;          /* Tracer.Seed (0 is a valid fixed seed here; the Go "0 = random" is host policy) */
+    int32_t y_start;
+    int32_t y_end;
+    int32_t tile_rows;  /* 0 = every row of [y_start, y_end) */
+    int32_t tile_count; /* >= 1 when tile_rows > 0 */
+    int32_t tile_index; /* 0 <= tile_index < tile_count */
+    int32_t output;     /* tray_output */
+} tray_params;
+
+typedef struct tray_scene_s *tray_scene_t;
+
+/* ---- discovery / lifetime ------------------------------------------------ */
+int32_t tray_abi_version(void);
+const char *tray_last_error(void);
+/* Number of usable gfx950 devices (0 when none). */
+int tray_device_count(int32_t *count);
+/* Free every library-owned device buffer on every device. */
+int tray_shutdown(void);
+
+/* ---- host-side setup (ray/camera.go, ray/objects.go) ------------------------ */
+/* Camera.Initialize (ray/camera.go:43-105): applies zero-field defaults to
+ * *setup in place (as the Go method mutates its receiver) and writes *out. */
+int tray_camera_initialize(tray_camera_setup *setup, int32_t width, int32_t height, tray_camera *out);
+/* RichSceneCamera (ray/camera.go:144-154). */
+int tray_rich_scene_camera(tray_camera_setup *out);
+/* DefaultBackground (ray/objects.go:106-110). */
+int tray_default_background(tray_background *out);
+/* DefaultScene (ray/objects.go:112-130): writes 5 spheres. */
+int tray_default_scene(tray_sphere *out, int32_t capacity, int32_t *count);
+/* RichScene (ray/objects.go:132-175) drawn from the counter RNG stream
+ * (purpose 4). half_extent = 11 is the book-cover grid; larger values give the
+ * dense variant used for the ~2000-sphere config. */
+int tray_rich_scene(uint64_t seed, int32_t half_extent, tray_sphere *out, int32_t capacity, int32_t *count);
+/* Upper bound of spheres tray_rich_scene can produce for half_extent. */
+int32_t tray_rich_scene_capacity(int32_t half_extent);
+
+/* ---- the hot path -------------------------------------------------------------- */
+/* Synchronous drop-in for Tracer.RenderLines (ray/tracer.go:120-155) over the
+ * row set in *params: uploads the scene, renders on `device`, and copies the
+ * compact rows into caller-owned host memory `out` (size: rows x width x
+ * bytes-per-pixel of params->output). `segments_out` (nullable) receives the
+ * per-pixel count of Scene.Hit calls summed over samples (uint32). */
+int tray_render(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
+                const tray_camera *camera, const tray_params *params, int32_t device, void *out,
+                uint32_t *segments_out);
+
+/* Device-resident scene for repeated renders (the scene is read-only during
+ * Render, ray/tracer.go:48). */
+int tray_scene_upload(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
+                      int32_t device, tray_scene_t *out);
+int tray_scene_release(tray_scene_t scene);
+
+/* Asynchronous render into DEVICE memory on `stream` (a hipStream_t, or NULL for
+ * the null stream of the scene's device). out_device: compact rows in the
+ * params->output format; segments_device nullable. Returns after enqueueing. */
+int tray_render_async(tray_scene_t scene, const tray_camera *camera, const tray_params *params, void *out_device,
+                      uint32_t *segments_device, void *stream);
+
+/* Rows rendered by *params (size of the compact output in rows). */
+int32_t tray_params_rows(const tray_params *params);
+
+/* ColorF.ToSRGBA on the host (ray/vec3.go:173-180): n_pixels linear RGB doubles -> RGBA8. */
+int tray_to_srgba(const double *rgb, size_t n_pixels, uint8_t *rgba);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRAY_H */

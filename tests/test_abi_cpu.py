@@ -1,0 +1,170 @@
+"""C-ABI on the CPU: the library loads, exports every symbol include/tray.h
+declares, its host-side setup matches the oracle bit for bit, argument errors
+are reported before any device work, and without a GPU it fails loudly (no
+fallback). No kernel is launched here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def test_exports_match_header(L):
+    header = open(os.path.join(ROOT, "include", "tray.h")).read()
+    declared = set(re.findall(r"^(?:int|int32_t|const char \*)\s*\**\s*(tray_\w+)\(", header, re.M))
+    assert declared == set(L.EXPORTS)
+    lib = L.lib()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.tray_abi_version() == 1
+
+
+def _setup(L, arr):
+    d3 = ctypes.c_double * 3
+    return L.CameraSetup(d3(*arr[0:3]), d3(*arr[3:6]), d3(*arr[6:9]), *arr[9:13])
+
+
+@pytest.mark.parametrize(
+    "setup,w,h",
+    [
+        (np.array([13, 2, 3, 0, 0, 0, 0, 1, 0, 20.0, 10.0, 10.0, 0.1]), 1280, 720),
+        (np.zeros(13), 100, 100),
+        (np.array([1, 2, 3, 1, 2, 3, 0, 0, 0, 0, 0, 0, 0.0]), 64, 48),
+        (np.array([-2, 2, 1, 0, 0, -1, 0, 0, 0, 20.0, 0, 3.0, 0.1]), 400, 225),
+        (np.array([0, 0, 5, 0, 0, 0, 0, 1, 0, 45.0, 2.0, 0, 0.5]), 33, 77),
+    ],
+)
+def test_camera_initialize_matches_oracle(L, O, setup, w, h):
+    cs = _setup(L, setup)
+    st = L.CameraState()
+    L.check(L.lib().tray_camera_initialize(ctypes.byref(cs), w, h, ctypes.byref(st)))
+    io, cam = O.camera_initialize(setup, w, h)
+    assert np.array_equal(st.as_array(), cam)
+    resolved = np.array([*cs.position, *cs.look_at, *cs.up, cs.vertical_fov, cs.focal_length, cs.focus_distance,
+                         cs.aperture])
+    assert np.array_equal(resolved, io)
+
+
+@pytest.mark.parametrize("seed,half", [(2, 11), (7, 11), (42, 11), (7, 22), (1, 0)])
+def test_rich_scene_matches_oracle(O, seed, half):
+    from tray_amd import ray
+
+    a = ray.rich_scene_array(seed, half)
+    b = O.rich_scene(seed, half)
+    assert a.tobytes() == b.tobytes()
+
+
+def test_default_scene_and_background(L, O):
+    from tray_amd import ray
+
+    a = ray.DefaultScene()
+    assert a.to_array().tobytes() == O.default_scene().tobytes()
+    bg = L.Background()
+    L.check(L.lib().tray_default_background(ctypes.byref(bg)))
+    assert tuple(bg.color_a) + tuple(bg.color_b) == (1.0, 1.0, 1.0, 0.4, 0.65, 1.0)
+
+
+def test_to_srgba_matches_oracle(L, O):
+    rng = np.random.default_rng(0)
+    rgb = np.concatenate([rng.random((3000, 3)), rng.random((300, 3)) * 0.004, np.array([[0.5, 1.0, 0.0]]),
+                          np.array([[-1.0, 2.0, np.nan]])])
+    out = np.zeros((len(rgb), 4), dtype=np.uint8)
+    L.check(L.lib().tray_to_srgba(rgb.ctypes.data, len(rgb), out.ctypes.data))
+    assert np.array_equal(out, O.to_srgba(rgb))
+
+
+@pytest.mark.parametrize("h,tile,world", [(720, 8, 8), (720, 8, 3), (37, 5, 4), (10, 16, 2), (5, 1, 20)])
+def test_params_rows_and_shard_rows(L, h, tile, world):
+    from tray_amd import shard
+
+    total = 0
+    seen = []
+    for r in range(world):
+        p = L.make_params(17, h, 10, 1, 0.5, 1, tile_rows=tile, tile_count=world, tile_index=r)
+        rows = shard.rows_for(h, tile, world, r)
+        assert L.params_rows(p) == len(rows)
+        total += len(rows)
+        seen.extend(rows.tolist())
+    assert total == h and sorted(seen) == list(range(h))
+    assert L.params_rows(L.make_params(17, h, 10, 1, 0.5, 1, y_start=2, y_end=h - 1)) == h - 3
+
+
+def _render_rc(L, spheres=None, **kw):
+    base = dict(width=8, height=8, max_depth=5, rays_per_pixel=1, ray_radius=0.5, seed=1)
+    base.update(kw)
+    p = L.make_params(**base)
+    bg = L.Background()
+    cam = L.CameraState()
+    s = L.spheres_array(spheres)
+    out = np.zeros(8 * 8 * 4 * 24, dtype=np.uint8)
+    return L.lib().tray_render(s.ctypes.data if len(s) else None, len(s), ctypes.byref(bg), ctypes.byref(cam),
+                               ctypes.byref(p), 0, out.ctypes.data, None)
+
+
+@pytest.mark.parametrize(
+    "kw",
+    [dict(width=0), dict(height=-1), dict(max_depth=0), dict(rays_per_pixel=0), dict(ray_radius=float("inf")),
+     dict(y_start=5, y_end=3), dict(y_end=9), dict(tile_rows=4, tile_count=2, tile_index=2), dict(tile_rows=-1),
+     dict(output=7)],
+)
+def test_invalid_params_rejected_before_device(L, kw):
+    assert _render_rc(L, **kw) == L.TRAY_ERR_INVALID_ARGUMENT
+    assert L.lib().tray_last_error()
+
+
+def test_unsupported_material(L):
+    s = np.zeros(2, dtype=L.SPHERE_DTYPE)
+    s["material"] = [1, 9]
+    assert _render_rc(L, s) == L.TRAY_ERR_UNSUPPORTED
+    assert b"unsupported material" in L.lib().tray_last_error()
+
+
+def test_too_many_pixels(L):
+    assert _render_rc(L, width=70000, height=70000) == L.TRAY_ERR_TOO_LARGE
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is present")
+def test_no_device_fails_loudly(L):
+    assert _render_rc(L) == L.TRAY_ERR_NO_DEVICE
+    n = ctypes.c_int32(-1)
+    assert L.lib().tray_device_count(ctypes.byref(n)) == 0 and n.value == 0
+
+
+def test_go_api_defaults_without_gpu():
+    """ray/tracer_test.go:108-170 defaulting + camera_test.go defaults via the mirror (host only)."""
+    from tray_amd import ray
+
+    t = ray.New(5, 5)
+    sc = t._apply_defaults(ray.DefaultScene())
+    t.Camera.Initialize(5, 5)
+    assert (t.FocalLength, t.VerticalFoV, t.MaxDepth, t.NumRaysPerPixel, t.RayRadius) == (1.0, 90.0, 10, 1, 0.5)
+    assert t.NumWorkers == (os.cpu_count() or 1)
+    assert sc.Background == ray.DefaultBackground()
+    t = ray.New(5, 5)
+    t.Position, t.FocalLength, t.VerticalFoV = (1, 2, 3), 10, 45.0
+    t.MaxDepth, t.NumRaysPerPixel, t.RayRadius, t.NumWorkers = 20, 4, 1.0, 2
+    t._apply_defaults(ray.DefaultScene())
+    t.Camera.Initialize(5, 5)
+    assert (t.Position, t.FocalLength, t.VerticalFoV, t.MaxDepth, t.NumRaysPerPixel, t.RayRadius, t.NumWorkers) == (
+        (1.0, 2.0, 3.0), 10, 45.0, 20, 4, 1.0, 2)
+    t = ray.New(10, 10)
+    t._apply_defaults(None)  # Render(nil): DefaultScene + its camera (tracer.go:50-62)
+    assert t.Position == (-2.0, 2.0, 1.0) and t.Aperture == 0.1 and t.VerticalFoV == 20.0
+    assert t.FocusDistance == 12.0 ** 0.5  # Length(Sub(Position, LookAt)) = |(-2, 2, 2)|
+
+
+def test_scene_flattening_errors():
+    from tray_amd import _lib, ray
+
+    class Weird:
+        pass
+
+    with pytest.raises(_lib.TrayError):
+        ray.Scene([ray.Sphere((0, 0, 0), 1, Weird())]).to_array()
+    with pytest.raises(_lib.TrayError):
+        ray.Scene([Weird()]).to_array()
+    arr = ray.Scene([ray.Sphere((0, 0, -1), 0.5, ray.Metal((0.8, 0.8, 0.8), 0.3))]).to_array()
+    assert arr["material"][0] == _lib.METAL and arr["param"][0] == 0.3

@@ -1,0 +1,177 @@
+"""HIP megakernel (through the C-ABI) vs the oracle and the golden fixtures.
+
+Parity bar: per-pixel Scene.Hit counts bit-exact (every path decision equal);
+linear mean colour within 1e-4 L-inf (BASELINE.json north star), and in
+practice within 1e-12: the only arithmetic difference is the attenuation
+product order (kernel outer-first, Go recursion inner-first)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import DEFAULT_BG, RICH_SETUP, load_golden
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4        # north-star gate (BASELINE.json)
+TIGHT = 1e-12     # observed: product-order ulps only
+WORKERS = min(16, os.cpu_count() or 4)
+
+
+def camera(L, setup, w, h):
+    d3 = ctypes.c_double * 3
+    cs = L.CameraSetup(d3(*setup[0:3]), d3(*setup[3:6]), d3(*setup[6:9]), *[float(v) for v in setup[9:13]])
+    st = L.CameraState()
+    L.check(L.lib().tray_camera_initialize(ctypes.byref(cs), w, h, ctypes.byref(st)))
+    return st
+
+
+def bg_struct(L, bg):
+    d3 = ctypes.c_double * 3
+    return L.Background(d3(*bg[0:3]), d3(*bg[3:6]))
+
+
+def gpu_render(L, spheres, bg, cam, w, h, spp, depth, radius, seed, **kw):
+    p = L.make_params(w, h, depth, spp, radius, seed, **kw)
+    return L.render(spheres, bg_struct(L, bg), cam, p, 0, segments=True)
+
+
+def check(gpu_rgb, gpu_seg, ref_rgb, ref_seg):
+    assert gpu_rgb.shape == ref_rgb.shape
+    assert np.array_equal(gpu_seg, ref_seg), f"{int((gpu_seg != ref_seg).sum())} pixels took different paths"
+    err = float(np.max(np.abs(gpu_rgb - ref_rgb))) if gpu_rgb.size else 0.0
+    assert err <= TOL
+    assert err <= TIGHT, err
+
+
+def test_device_present(L):
+    assert L.device_count() >= 1
+
+
+@pytest.mark.parametrize("name", ["rngfree_mirrors", "rngfree_mirrors_deep"])
+def test_rngfree_golden(L, name):
+    g = load_golden(name)
+    st = camera(L, g["camera_setup"], int(g["width"]), int(g["height"]))
+    assert np.array_equal(st.as_array(), g["camera"])
+    rgb, seg = gpu_render(L, g["spheres"], g["background"], st, int(g["width"]), int(g["height"]), 1,
+                          int(g["max_depth"]), 0.5, 77)
+    check(rgb, seg, g["rgb"], g["segments"])
+
+
+CASES = {
+    # name: (scene, setup, w, h, spp, depth, radius, seed)
+    "default_scene": ("default", np.array([-2, 2, 1, 0, 0, -1, 0, 0, 0, 20.0, 0, 12.0 ** 0.5, 0.1]), 48, 32, 8, 10,
+                      0.5, 1),
+    "book_seed2_dof": ("rich2", RICH_SETUP, 96, 54, 4, 50, 0.5, 2),
+    "book_r1_pinhole": ("rich2", np.r_[RICH_SETUP[:12], 0.0], 80, 45, 1, 50, 0.5, 3),
+    "book_radius1": ("rich2", RICH_SETUP, 40, 30, 6, 20, 1.0, 11),
+    "book_depth1": ("rich2", RICH_SETUP, 40, 30, 3, 1, 0.5, 4),
+    "dense_seed7": ("dense7", RICH_SETUP, 48, 27, 2, 50, 0.5, 7),
+    "empty": ("empty", RICH_SETUP, 33, 17, 4, 50, 0.5, 5),
+    "seed_zero_and_big": ("rich2", RICH_SETUP, 21, 13, 5, 50, 0.5, 0),
+    "seed_high_bits": ("rich2", RICH_SETUP, 21, 13, 5, 50, 0.5, 0xDEADBEEF12345678),
+}
+
+
+def scene_for(O, key):
+    return {"default": O.default_scene, "rich2": lambda: O.rich_scene(2), "dense7": lambda: O.rich_scene(7, 22),
+            "empty": lambda: O.default_scene()[:0]}[key]()
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_vs_oracle(L, O, case):
+    key, setup, w, h, spp, depth, radius, seed = CASES[case]
+    sc = scene_for(O, key)
+    st = camera(L, setup, w, h)
+    rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, depth, radius, seed)
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, spp, depth, radius, seed, workers=WORKERS)
+    check(rgb, seg, ref, rseg)
+
+
+def test_config1_full_size(L, O):
+    """BASELINE config 1 (the reference's benchmark/ invocation): 400x225, r=16, d=12, seed 2, full image."""
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, 400, 225)
+    rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, 400, 225, 16, 12, 0.5, 2)
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), 400, 225, 16, 12, 0.5, 2, workers=WORKERS)
+    check(rgb, seg, ref, rseg)
+
+
+def test_row_range_and_tiles_are_partition_invariant(L, O):
+    sc = O.rich_scene(2)
+    w, h = 64, 37
+    st = camera(L, RICH_SETUP, w, h)
+    full, fseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 3, 50, 0.5, 8)
+    part, pseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 3, 50, 0.5, 8, y_start=5, y_end=21)  # RenderLines rows
+    assert np.array_equal(part, full[5:21]) and np.array_equal(pseg, fseg[5:21])
+    from tray_amd import shard
+
+    for world, tile in [(3, 5), (2, 1), (4, 16), (8, 8)]:
+        got = np.zeros_like(full)
+        for r in range(world):
+            out, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 3, 50, 0.5, 8, tile_rows=tile, tile_count=world,
+                                tile_index=r)
+            got[shard.rows_for(h, tile, world, r)] = out
+        assert np.array_equal(got, full)
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, 3, 50, 0.5, 8, workers=WORKERS)
+    check(full, fseg, ref, rseg)
+
+
+def test_output_formats(L, O):
+    sc = O.rich_scene(2)
+    w, h = 50, 28
+    st = camera(L, RICH_SETUP, w, h)
+    f64, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 4, 50, 0.5, 3)
+    f32, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 4, 50, 0.5, 3, output=L.OUT_RGB_F32)
+    assert f32.dtype == np.float32 and np.array_equal(f32, f64.astype(np.float32))
+    u8, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 4, 50, 0.5, 3, output=L.OUT_RGBA8)
+    host = O.to_srgba(f64)
+    d = np.abs(u8.astype(int) - host.astype(int))
+    assert np.all(u8[..., 3] == 255) and d.max() <= 1 and (d == 0).mean() >= 0.999
+
+
+def test_scene_larger_than_lds(L, O):
+    """> 5120 spheres: the kernel reads geometry from global memory instead of LDS."""
+    sc = O.rich_scene(5, 40)
+    assert len(sc) * 32 > 160 * 1024
+    st = camera(L, RICH_SETUP, 24, 14)
+    rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, 24, 14, 2, 12, 0.5, 6)
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), 24, 14, 2, 12, 0.5, 6, workers=WORKERS)
+    check(rgb, seg, ref, rseg)
+
+
+def test_ragged_and_tiny_images(L, O):
+    sc = O.default_scene()
+    for w, h in [(1, 1), (1, 17), (17, 1), (15, 15), (16, 16), (17, 33)]:
+        st = camera(L, np.array([-2, 2, 1, 0, 0, -1, 0, 0, 0, 20.0, 0, 3.0, 0.1]), w, h)
+        rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 3, 10, 0.5, 2)
+        ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, 3, 10, 0.5, 2)
+        check(rgb, seg, ref, rseg)
+
+
+def test_example_png_sky_rows(L, O):
+    rows = load_golden("example_sky_rows")["rows"]
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, 1280, 720)
+    u8, seg = gpu_render(L, sc, DEFAULT_BG, st, 1280, 720, 64, 50, 0.5, 2, y_start=0, y_end=49,
+                         output=L.OUT_RGBA8)
+    assert np.all(seg == 64)
+    d = np.abs(u8[..., :3].astype(int) - rows.astype(int))
+    assert d.max() <= 1 and (d.max(-1) == 0).mean() >= 0.98
+
+
+def test_config2_full_size_properties(L, O):
+    """BASELINE config 2 at full size (1280x720, r=64, d=50): determinism, and a
+    random spot-check of pixels against the oracle (size-independent parity)."""
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, 1280, 720)
+    a, sa = gpu_render(L, sc, DEFAULT_BG, st, 1280, 720, 64, 50, 0.5, 2)
+    b, sb = gpu_render(L, sc, DEFAULT_BG, st, 1280, 720, 64, 50, 0.5, 2)
+    assert np.array_equal(a, b) and np.array_equal(sa, sb)
+    rng = np.random.default_rng(2)
+    xs = rng.integers(0, 1280, 96)
+    ys = np.concatenate([rng.integers(0, 720, 64), rng.integers(400, 720, 32)])  # extra ground pixels
+    ref, rseg = O.render_pixels(sc, DEFAULT_BG, st.as_array(), 1280, 720, 64, 50, 0.5, 2, xs, ys)
+    check(a[ys, xs], sa[ys, xs], ref, rseg)
+    assert sa.min() >= 64 and sa.max() <= 64 * 50

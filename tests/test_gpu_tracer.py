@@ -1,0 +1,101 @@
+"""fortio/tray ray/tracer_test.go and camera_test.go:245-283, run against the
+Go-API mirror (tray_amd.ray) whose Render/RenderLines go through the HIP path."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ray():
+    from tray_amd import ray
+
+    return ray
+
+
+def test_render_default_scene(ray):  # tracer_test.go:47-78
+    t = ray.New(10, 10)
+    t.Seed = 1
+    img = t.Render(None)
+    assert img is t.imageData and img.shape == (10, 10, 4)
+    assert np.all(img[..., 3] == 255) and np.any(img[..., :3] != 0)
+
+
+def test_render_custom_scene_alpha(ray):  # tracer_test.go:80-106
+    t = ray.New(5, 5)
+    img = t.Render(ray.Scene([ray.Sphere((0, 0, -1), 0.5, ray.Lambertian((1, 0, 0)))]))
+    assert np.all(img[..., 3] == 255)
+
+
+def test_render_default_and_custom_parameters(ray):  # tracer_test.go:108-170
+    import os
+
+    t = ray.New(5, 5)
+    t.Render(ray.DefaultScene())
+    assert (t.FocalLength, t.VerticalFoV, t.MaxDepth, t.NumRaysPerPixel, t.RayRadius) == (1.0, 90.0, 10, 1, 0.5)
+    assert t.NumWorkers == (os.cpu_count() or 1)
+    t = ray.New(5, 5)
+    t.Position, t.FocalLength, t.VerticalFoV = (1, 2, 3), 10, 45.0
+    t.MaxDepth, t.NumRaysPerPixel, t.RayRadius, t.NumWorkers = 20, 4, 1.0, 2
+    t.Render(ray.DefaultScene())
+    assert (t.Position, t.FocalLength, t.VerticalFoV, t.MaxDepth, t.NumRaysPerPixel, t.RayRadius, t.NumWorkers) == (
+        (1.0, 2.0, 3.0), 10, 45.0, 20, 4, 1.0, 2)
+
+
+def test_progress_total(ray):  # tracer_test.go:172-186
+    t = ray.New(10, 8)
+    total = []
+    t.ProgressFunc = total.append
+    t.Render(ray.DefaultScene())
+    assert sum(total) == 80
+
+
+@pytest.mark.parametrize("workers,w,h", [(1, 10, 10), (2, 10, 10), (20, 10, 5)])
+def test_parallel_rendering_all_pixels(ray, workers, w, h):  # tracer_test.go:188-222
+    t = ray.New(w, h)
+    t.NumWorkers = workers
+    img = t.Render(ray.DefaultScene())
+    assert np.all(img[..., 3] == 255)
+
+
+@pytest.mark.parametrize("n", [1, 4, 10])
+def test_multiple_rays_per_pixel(ray, n):  # tracer_test.go:224-256
+    t = ray.New(5, 5)
+    t.NumRaysPerPixel = n
+    assert np.all(t.Render(ray.DefaultScene())[..., 3] == 255)
+
+
+def test_render_lines(ray):  # tracer_test.go:258-297
+    t = ray.New(10, 10)
+    t.FocalLength, t.VerticalFoV, t.MaxDepth, t.NumRaysPerPixel, t.RayRadius = 5, 30.0, 10, 1, 0.5
+    scene = ray.DefaultScene()
+    t.Camera.Initialize(10, 10)
+    t.RenderLines(0, 0, 3, scene)
+    assert np.all(t.imageData[:3, :, 3] == 255)
+    assert np.all(t.imageData[3:] == 0)
+
+
+def test_render_empty_scene_is_sky(ray):  # tracer_test.go:299-321
+    t = ray.New(5, 5)
+    img = t.Render(ray.Scene([]))
+    assert np.all(img[..., 3] == 255) and np.all(img[..., 2] > 0)
+
+
+def test_rich_scene_not_black(ray):  # camera_test.go:245-283
+    t = ray.New(20, 20)
+    t.Camera = ray.RichSceneCamera()
+    t.MaxDepth, t.NumRaysPerPixel, t.Seed = 10, 2, 42
+    img = t.Render(ray.RichScene(42))
+    assert (img[..., :3].max(-1) > 0).sum() >= 200
+
+
+def test_seed_reproducible_and_sensitive(ray):  # Seed semantics (tracer.go:33)
+    def render(seed):
+        t = ray.New(16, 9)
+        t.Camera = ray.RichSceneCamera()
+        t.MaxDepth, t.NumRaysPerPixel, t.Seed = 12, 4, seed
+        t.Render(ray.RichScene(2))
+        return t.linear.copy()
+
+    a, b, c = render(5), render(5), render(6)
+    assert np.array_equal(a, b) and not np.array_equal(a, c)

@@ -1,0 +1,87 @@
+"""Oracle: sampler statistics (the reference's only pins on its sampler,
+ray/vec3_test.go:539-741), RNG-free golden scenes (independent numpy
+restatement, tests/golden/make_golden.py) and the sky of the reference's own
+example.png. CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import DEFAULT_BG, RICH_SETUP, load_golden
+
+
+def test_unit_vector_distribution(O):  # ray/vec3_test.go:539-649 (100k samples)
+    n = 100_000
+    v = np.array([O.unit_vector(42, i, i % 7, i % 50) for i in range(n)])
+    assert np.all(np.abs(v.mean(0)) <= 0.015)
+    assert np.all(np.abs(v.var(0) - 1.0 / 3.0) <= 0.01)
+    octant = (v[:, 0] > 0) * 4 + (v[:, 1] > 0) * 2 + (v[:, 2] > 0)
+    counts = np.bincount(octant, minlength=8)
+    assert np.all(np.abs(counts - n / 8) <= 0.15 * n / 8)
+    z_hist = np.histogram(v[:, 2], bins=20, range=(-1, 1))[0]  # Archimedes: z is uniform (vec3_test.go:651-705)
+    assert np.all(np.abs(z_hist - n / 20) <= 0.1 * n / 20)
+
+
+@pytest.mark.parametrize("purpose,radius", [(1, 0.5), (2, 1.0), (1, 1.0)])
+def test_in_disc(O, purpose, radius):  # InDisc: inside the disc, uniform over its area
+    d = np.array([O.in_disc(3, i, 0, purpose, radius) for i in range(40_000)])
+    r2 = (d**2).sum(1)
+    assert np.all(r2 < radius * radius)
+    assert abs(r2.mean() / (radius * radius) - 0.5) < 0.01  # E[r^2] = R^2/2 for a uniform disc
+    assert np.all(np.abs(d.mean(0)) < 0.01 * radius)
+
+
+@pytest.mark.parametrize("name", ["rngfree_mirrors", "rngfree_mirrors_deep"])
+def test_rngfree_golden(O, name):
+    g = load_golden(name)
+    io, cam = O.camera_initialize(g["camera_setup"], int(g["width"]), int(g["height"]))
+    assert np.array_equal(cam, g["camera"])
+    img, seg = O.render(g["spheres"], g["background"], g["camera"], int(g["width"]), int(g["height"]), 1,
+                        int(g["max_depth"]), 0.5, 12345)
+    assert np.array_equal(seg, g["segments"])
+    assert np.array_equal(img, g["rgb"])  # bit-exact: same op order, no RNG involved
+
+
+def test_example_png_sky_rows(O):
+    """Rows 0..48 of the reference's own output (1280x720, r=64, d=50, seed 2).
+    Pure sky, so camera + AmbientLight + LinearToSrgb are checked against the
+    real Go binary; the +-1 LSB is AA noise of a different random stream."""
+    rows = load_golden("example_sky_rows")["rows"]
+    _, cam = O.camera_initialize(RICH_SETUP, 1280, 720)
+    sc = O.rich_scene(2)
+    img, seg = O.render(sc, DEFAULT_BG, cam, 1280, 720, 64, 50, 0.5, 2, 0, 49, workers=os.cpu_count() or 4)
+    assert np.all(seg == 64)  # every sample escaped to the sky at its first segment
+    diff = np.abs(O.to_srgba(img)[..., :3].astype(int) - rows.astype(int))
+    assert diff.max() <= 1
+    assert (diff.max(-1) == 0).mean() >= 0.98
+    # pixel-centre rays through a pinhole: the analytic recomputation of SURVEY.md §8(c)
+    setup = RICH_SETUP.copy()
+    setup[12] = 0.0
+    _, cam0 = O.camera_initialize(setup, 1280, 720)
+    img0, _ = O.render(None, DEFAULT_BG, cam0, 1280, 720, 1, 50, 0.5, 2, 0, 49)
+    d0 = np.abs(O.to_srgba(img0)[..., :3].astype(int) - rows.astype(int)).max(-1)
+    assert d0.max() <= 1 and (d0 == 0).mean() >= 0.985
+
+
+def test_oracle_workers_invariant(O):
+    """The counter RNG removes the reference's -w dependence (ray/tracer.go:93,121)."""
+    _, cam = O.camera_initialize(RICH_SETUP, 40, 24)
+    sc = O.rich_scene(2)
+    a, sa = O.render(sc, DEFAULT_BG, cam, 40, 24, 3, 12, 0.5, 9, workers=1)
+    b, sb = O.render(sc, DEFAULT_BG, cam, 40, 24, 3, 12, 0.5, 9, workers=5)
+    assert np.array_equal(a, b) and np.array_equal(sa, sb)
+
+
+def test_rich_scene_structure(O):  # ray/objects.go:132-175; benchmark/benchmark.go:42 (486 objects @ seed 7)
+    for seed in (2, 7, 42):
+        sc = O.rich_scene(seed)
+        assert 4 < len(sc) <= 488
+        assert sc[0]["radius"] == 1000 and tuple(sc[0]["center"]) == (0, -1000, 0)
+        small = sc[1:-3]
+        assert np.all(small["radius"] == 0.2) and np.all(small["center"][:, 1] == 0.2)
+        assert np.all(np.linalg.norm(small["center"] - np.array([4, 0.2, 0]), axis=1) > 0.9)
+        mats = np.bincount(small["material"], minlength=4)[1:]
+        assert mats[0] > mats[1] > mats[2] > 0  # ~80 / 15 / 5 %
+        assert tuple(sc[-3]["center"]) == (0, 1, 0) and sc[-3]["material"] == 3
+    dense = O.rich_scene(7, 22)
+    assert 1800 < len(dense) <= 44 * 44 + 4

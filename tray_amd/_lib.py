@@ -1,0 +1,232 @@
+"""ctypes binding of the C-ABI in include/tray.h (libtray_amd.so, built in-tree).
+
+This is the only way the Python host reaches the renderer: there is no Python,
+PyTorch or CPU fallback for the hot path. If the shared library is missing the
+import fails loudly with the build command to run.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtray_amd.so")
+
+# include/tray.h enums
+TRAY_OK = 0
+TRAY_ERR_INVALID_ARGUMENT = -1
+TRAY_ERR_UNSUPPORTED = -2
+TRAY_ERR_DEVICE = -3
+TRAY_ERR_NO_DEVICE = -4
+TRAY_ERR_TOO_LARGE = -5
+LAMBERTIAN, METAL, DIELECTRIC = 1, 2, 3
+OUT_RGB_F64, OUT_RGB_F32, OUT_RGBA8 = 0, 1, 2
+BYTES_PER_PIXEL = {OUT_RGB_F64: 24, OUT_RGB_F32: 12, OUT_RGBA8: 4}
+
+# tray_sphere as a numpy structured dtype (72 bytes, C layout).
+SPHERE_DTYPE = np.dtype(
+    [
+        ("center", "<f8", (3,)),
+        ("radius", "<f8"),
+        ("albedo", "<f8", (3,)),
+        ("param", "<f8"),
+        ("material", "<i4"),
+        ("reserved", "<i4"),
+    ]
+)
+assert SPHERE_DTYPE.itemsize == 72
+
+_d3 = ctypes.c_double * 3
+
+
+class Background(ctypes.Structure):
+    _fields_ = [("color_a", _d3), ("color_b", _d3)]
+
+
+class CameraSetup(ctypes.Structure):
+    _fields_ = [
+        ("position", _d3),
+        ("look_at", _d3),
+        ("up", _d3),
+        ("vertical_fov", ctypes.c_double),
+        ("focal_length", ctypes.c_double),
+        ("focus_distance", ctypes.c_double),
+        ("aperture", ctypes.c_double),
+    ]
+
+
+class CameraState(ctypes.Structure):
+    _fields_ = [
+        ("position", _d3),
+        ("pixel00", _d3),
+        ("pixel_x", _d3),
+        ("pixel_y", _d3),
+        ("defocus_u", _d3),
+        ("defocus_v", _d3),
+        ("aperture", ctypes.c_double),
+        ("focus_distance", ctypes.c_double),
+        ("focal_length", ctypes.c_double),
+    ]
+
+    def as_array(self) -> np.ndarray:
+        """The 21 doubles in declaration order (the oracle's camera layout)."""
+        return np.frombuffer(bytes(self), dtype=np.float64).copy()
+
+
+assert ctypes.sizeof(CameraState) == 21 * 8
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("max_depth", ctypes.c_int32),
+        ("rays_per_pixel", ctypes.c_int32),
+        ("ray_radius", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+        ("y_start", ctypes.c_int32),
+        ("y_end", ctypes.c_int32),
+        ("tile_rows", ctypes.c_int32),
+        ("tile_count", ctypes.c_int32),
+        ("tile_index", ctypes.c_int32),
+        ("output", ctypes.c_int32),
+    ]
+
+
+class TrayError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"tray error {code}: {message}")
+        self.code = code
+
+
+# Every symbol include/tray.h declares (tests check the library exports all of them).
+EXPORTS = (
+    "tray_abi_version",
+    "tray_last_error",
+    "tray_device_count",
+    "tray_shutdown",
+    "tray_camera_initialize",
+    "tray_rich_scene_camera",
+    "tray_default_background",
+    "tray_default_scene",
+    "tray_rich_scene",
+    "tray_rich_scene_capacity",
+    "tray_render",
+    "tray_scene_upload",
+    "tray_scene_release",
+    "tray_render_async",
+    "tray_params_rows",
+    "tray_to_srgba",
+)
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: the HIP renderer is not built. Run `make -C tray_amd` "
+            "(or __graft_entry__.build()). There is no CPU fallback."
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, u32p = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32)
+    L.tray_abi_version.restype = i32
+    L.tray_last_error.restype = ctypes.c_char_p
+    L.tray_device_count.argtypes = [ctypes.POINTER(i32)]
+    L.tray_camera_initialize.argtypes = [ctypes.POINTER(CameraSetup), i32, i32, ctypes.POINTER(CameraState)]
+    L.tray_rich_scene_camera.argtypes = [ctypes.POINTER(CameraSetup)]
+    L.tray_default_background.argtypes = [ctypes.POINTER(Background)]
+    L.tray_default_scene.argtypes = [vp, i32, ctypes.POINTER(i32)]
+    L.tray_rich_scene.argtypes = [ctypes.c_uint64, i32, vp, i32, ctypes.POINTER(i32)]
+    L.tray_rich_scene_capacity.argtypes = [i32]
+    L.tray_rich_scene_capacity.restype = i32
+    L.tray_render.argtypes = [vp, i32, ctypes.POINTER(Background), ctypes.POINTER(CameraState),
+                              ctypes.POINTER(Params), i32, vp, u32p]
+    L.tray_scene_upload.argtypes = [vp, i32, ctypes.POINTER(Background), i32, ctypes.POINTER(vp)]
+    L.tray_scene_release.argtypes = [vp]
+    L.tray_render_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
+    L.tray_params_rows.argtypes = [ctypes.POINTER(Params)]
+    L.tray_params_rows.restype = i32
+    L.tray_to_srgba.argtypes = [vp, ctypes.c_size_t, vp]
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != TRAY_OK:
+        msg = lib().tray_last_error()
+        raise TrayError(rc, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    check(lib().tray_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def spheres_array(spheres) -> np.ndarray:
+    a = np.ascontiguousarray(spheres if spheres is not None else np.zeros(0, SPHERE_DTYPE))
+    if a.dtype != SPHERE_DTYPE:
+        raise TypeError("spheres must use tray_amd._lib.SPHERE_DTYPE")
+    return a
+
+
+def make_params(width, height, max_depth, rays_per_pixel, ray_radius, seed, y_start=0, y_end=None,
+                tile_rows=0, tile_count=1, tile_index=0, output=OUT_RGB_F64) -> Params:
+    return Params(width, height, max_depth, rays_per_pixel, float(ray_radius), int(seed) & (2**64 - 1), y_start,
+                  height if y_end is None else y_end, tile_rows, tile_count, tile_index, output)
+
+
+def params_rows(p: Params) -> int:
+    return int(lib().tray_params_rows(ctypes.byref(p)))
+
+
+def render(spheres, background: Background, camera: CameraState, params: Params, device: int = 0,
+           segments: bool = False):
+    """Synchronous tray_render into host memory. Returns (pixels, segments-or-None);
+    pixels is (rows, W, 3) f64 / (rows, W, 3) f32 / (rows, W, 4) u8 by params.output."""
+    s = spheres_array(spheres)
+    rows = params_rows(params)
+    shape = {OUT_RGB_F64: (rows, params.width, 3), OUT_RGB_F32: (rows, params.width, 3),
+             OUT_RGBA8: (rows, params.width, 4)}[params.output]
+    dtype = {OUT_RGB_F64: np.float64, OUT_RGB_F32: np.float32, OUT_RGBA8: np.uint8}[params.output]
+    out = np.zeros(shape, dtype=dtype)
+    seg = np.zeros((rows, params.width), dtype=np.uint32) if segments else None
+    check(lib().tray_render(s.ctypes.data if len(s) else None, len(s), ctypes.byref(background),
+                            ctypes.byref(camera), ctypes.byref(params), device, out.ctypes.data,
+                            seg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) if seg is not None else None))
+    return out, seg
+
+
+class DeviceScene:
+    """A scene uploaded once to one device (tray_scene_upload); render many times."""
+
+    def __init__(self, spheres, background: Background, device: int = 0):
+        s = spheres_array(spheres)
+        h = ctypes.c_void_p()
+        check(lib().tray_scene_upload(s.ctypes.data if len(s) else None, len(s), ctypes.byref(background), device,
+                                      ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+        self.n = len(s)
+
+    def render_async(self, camera: CameraState, params: Params, out_ptr: int, segments_ptr: int | None = None,
+                     stream: int | None = None) -> None:
+        check(lib().tray_render_async(self.handle, ctypes.byref(camera), ctypes.byref(params), out_ptr,
+                                      segments_ptr, stream))
+
+    def release(self) -> None:
+        if self.handle:
+            lib().tray_scene_release(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass

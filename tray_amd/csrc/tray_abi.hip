@@ -1,0 +1,332 @@
+// tray_abi.hip — the C-ABI (include/tray.h) around the megakernel.
+//
+// Replaces the hot half of (*Tracer).Render / RenderLines (ray/tracer.go:48-155):
+// scene flattening + upload, one kernel launch per row set, copy-out. The Go
+// host's defaulting (ray/tracer.go:50-84) happens BEFORE these calls, in the
+// caller (tray_amd/ray.py or a cgo shim), exactly as Render does it.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <cmath>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/tray.h"
+#include "tray_internal.hpp"
+#include "tray_kernel.hpp"
+
+namespace tray {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+static int hip_fail(hipError_t e, const char* what) {
+    return fail(TRAY_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define TRAY_HIP(call)                                  \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+
+struct DeviceState {
+    std::mutex mu;
+    bool checked = false;
+    bool usable = false;
+    hipStream_t stream = nullptr;
+    void* out_ws = nullptr;
+    size_t out_ws_bytes = 0;
+    uint32_t* seg_ws = nullptr;
+    size_t seg_ws_bytes = 0;
+};
+
+static std::mutex g_devices_mu;
+static std::vector<DeviceState*> g_devices;
+
+static int visible_devices(int* count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) {
+        *count = 0;
+        return TRAY_OK;
+    }
+    *count = n;
+    return TRAY_OK;
+}
+
+static int device_state(int32_t device, DeviceState** out) {
+    int n = 0;
+    visible_devices(&n);
+    if (n <= 0) return fail(TRAY_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(TRAY_ERR_INVALID_ARGUMENT, "device ordinal out of range");
+    std::lock_guard<std::mutex> lk(g_devices_mu);
+    if ((int)g_devices.size() < n) g_devices.resize(n, nullptr);
+    if (!g_devices[device]) g_devices[device] = new DeviceState();
+    DeviceState* st = g_devices[device];
+    if (!st->checked) {
+        hipDeviceProp_t prop;
+        TRAY_HIP(hipGetDeviceProperties(&prop, device));
+        st->usable = strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+        st->checked = true;
+        if (!st->usable)
+            return fail(TRAY_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+    }
+    if (!st->usable) return fail(TRAY_ERR_NO_DEVICE, "device is not gfx950");
+    *out = st;
+    return TRAY_OK;
+}
+
+}  // namespace tray
+
+struct tray_scene_s {
+    int32_t device;
+    int32_t n;
+    double4* geo;
+    tray::MatRec* mat;
+    tray::V3 bg_a, bg_b;
+};
+
+using namespace tray;
+
+static int validate_spheres(const tray_sphere* s, int32_t n) {
+    if (n < 0) return fail(TRAY_ERR_INVALID_ARGUMENT, "negative sphere count");
+    if (n > 0 && !s) return fail(TRAY_ERR_INVALID_ARGUMENT, "null sphere array");
+    for (int32_t i = 0; i < n; ++i) {
+        if (s[i].material < TRAY_LAMBERTIAN || s[i].material > TRAY_DIELECTRIC)
+            return fail(TRAY_ERR_UNSUPPORTED, "sphere " + std::to_string(i) + ": unsupported material kind " +
+                                                  std::to_string(s[i].material));
+    }
+    return TRAY_OK;
+}
+
+static int validate_params(const tray_params* p) {
+    if (!p) return fail(TRAY_ERR_INVALID_ARGUMENT, "null params");
+    if (p->width <= 0 || p->height <= 0) return fail(TRAY_ERR_INVALID_ARGUMENT, "width/height must be > 0");
+    if ((uint64_t)p->width * (uint64_t)p->height > 0xFFFFFFFFull)
+        return fail(TRAY_ERR_TOO_LARGE, "image has more than 2^32 pixels (RNG pixel counter is 32-bit)");
+    if (p->max_depth <= 0) return fail(TRAY_ERR_INVALID_ARGUMENT, "max_depth must be > 0 (Render defaults it to 10)");
+    if (p->rays_per_pixel <= 0)
+        return fail(TRAY_ERR_INVALID_ARGUMENT, "rays_per_pixel must be > 0 (Render defaults it to 1)");
+    if (!std::isfinite(p->ray_radius)) return fail(TRAY_ERR_INVALID_ARGUMENT, "ray_radius must be finite");
+    if (p->y_start < 0 || p->y_end > p->height || p->y_start > p->y_end)
+        return fail(TRAY_ERR_INVALID_ARGUMENT, "row range outside the image");
+    if (p->tile_rows < 0) return fail(TRAY_ERR_INVALID_ARGUMENT, "tile_rows must be >= 0");
+    if (p->tile_rows > 0 && (p->tile_count < 1 || p->tile_index < 0 || p->tile_index >= p->tile_count))
+        return fail(TRAY_ERR_INVALID_ARGUMENT, "tile_index must be in [0, tile_count)");
+    if (p->output < TRAY_OUT_RGB_F64 || p->output > TRAY_OUT_RGBA8)
+        return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown output format");
+    return TRAY_OK;
+}
+
+static size_t bytes_per_pixel(int32_t fmt) {
+    return fmt == TRAY_OUT_RGB_F64 ? 24 : fmt == TRAY_OUT_RGB_F32 ? 12 : 4;
+}
+
+extern "C" {
+#pragma GCC visibility push(default)
+
+int32_t tray_abi_version(void) { return TRAY_ABI_VERSION; }
+
+const char* tray_last_error(void) { return g_last_error.c_str(); }
+
+int tray_device_count(int32_t* count) {
+    if (!count) return fail(TRAY_ERR_INVALID_ARGUMENT, "null count");
+    int n = 0;
+    visible_devices(&n);
+    int usable = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++usable;
+    }
+    *count = usable;
+    return TRAY_OK;
+}
+
+int32_t tray_params_rows(const tray_params* p) {
+    if (!p || p->y_end <= p->y_start) return 0;
+    const int32_t total = p->y_end - p->y_start;
+    if (p->tile_rows <= 0) return total;
+    if (p->tile_count < 1 || p->tile_index < 0 || p->tile_index >= p->tile_count) return 0;
+    const int32_t ntiles = (total + p->tile_rows - 1) / p->tile_rows;
+    int32_t rows = 0;
+    for (int32_t t = p->tile_index; t < ntiles; t += p->tile_count) {
+        const int32_t left = total - t * p->tile_rows;
+        rows += left < p->tile_rows ? left : p->tile_rows;
+    }
+    return rows;
+}
+
+int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_background* bg, int32_t device,
+                      tray_scene_t* out) {
+    if (!out || !bg) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    int rc = validate_spheres(spheres, n);
+    if (rc) return rc;
+    DeviceState* st = nullptr;
+    rc = device_state(device, &st);
+    if (rc) return rc;
+    TRAY_HIP(hipSetDevice(device));
+    std::vector<double4> geo((size_t)n);
+    std::vector<MatRec> mat((size_t)n);
+    for (int32_t i = 0; i < n; ++i) {
+        const tray_sphere& s = spheres[i];
+        // R*R precomputed: identical bits to Sphere.Hit's s.Radius*s.Radius (ray/objects.go:85).
+        geo[i] = make_double4(s.center[0], s.center[1], s.center[2], s.radius * s.radius);
+        MatRec& m = mat[i];
+        m.albedo[0] = s.albedo[0];
+        m.albedo[1] = s.albedo[1];
+        m.albedo[2] = s.albedo[2];
+        m.param = s.param;
+        m.radius = s.radius;
+        m.type = s.material;
+        m.pad = 0;
+    }
+    tray_scene_s* sc = new tray_scene_s();
+    sc->device = device;
+    sc->n = n;
+    sc->geo = nullptr;
+    sc->mat = nullptr;
+    sc->bg_a = V3{bg->color_a[0], bg->color_a[1], bg->color_a[2]};
+    sc->bg_b = V3{bg->color_b[0], bg->color_b[1], bg->color_b[2]};
+    if (n > 0) {
+        hipError_t e = hipMalloc(&sc->geo, sizeof(double4) * (size_t)n);
+        if (e == hipSuccess) e = hipMalloc(&sc->mat, sizeof(MatRec) * (size_t)n);
+        if (e == hipSuccess) e = hipMemcpy(sc->geo, geo.data(), sizeof(double4) * (size_t)n, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(sc->geo);
+            (void)hipFree(sc->mat);
+            delete sc;
+            return hip_fail(e, "scene upload");
+        }
+    }
+    *out = sc;
+    return TRAY_OK;
+}
+
+int tray_scene_release(tray_scene_t sc) {
+    if (!sc) return TRAY_OK;
+    (void)hipSetDevice(sc->device);
+    if (sc->geo) (void)hipFree(sc->geo);
+    if (sc->mat) (void)hipFree(sc->mat);
+    delete sc;
+    return TRAY_OK;
+}
+
+int tray_render_async(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
+                      uint32_t* segments_device, void* stream) {
+    if (!sc || !cam || !out_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+    int rc = validate_params(p);
+    if (rc) return rc;
+    KernelParams k;
+    memset(&k, 0, sizeof(k));
+    k.geo = sc->geo;
+    k.mat = sc->mat;
+    k.n = sc->n;
+    k.width = p->width;
+    k.height = p->height;
+    k.spp = p->rays_per_pixel;
+    k.max_depth = p->max_depth;
+    k.y_start = p->y_start;
+    k.rows = tray_params_rows(p);
+    k.tile_rows = p->tile_rows;
+    k.tile_count = p->tile_rows > 0 ? p->tile_count : 1;
+    k.tile_index = p->tile_rows > 0 ? p->tile_index : 0;
+    k.out_format = p->output;
+    k.ray_radius = p->ray_radius;
+    k.focus_time = cam->focus_distance / cam->focal_length;  // ray/camera.go:134
+    k.seed = p->seed;
+    memcpy(k.cam.position, cam->position, sizeof(k.cam.position));
+    memcpy(k.cam.pixel00, cam->pixel00, sizeof(k.cam.pixel00));
+    memcpy(k.cam.pixel_x, cam->pixel_x, sizeof(k.cam.pixel_x));
+    memcpy(k.cam.pixel_y, cam->pixel_y, sizeof(k.cam.pixel_y));
+    memcpy(k.cam.defocus_u, cam->defocus_u, sizeof(k.cam.defocus_u));
+    memcpy(k.cam.defocus_v, cam->defocus_v, sizeof(k.cam.defocus_v));
+    k.cam.aperture = cam->aperture;
+    k.bg_a = sc->bg_a;
+    k.bg_b = sc->bg_b;
+    k.out = out_device;
+    k.segments = segments_device;
+    TRAY_HIP(hipSetDevice(sc->device));
+    TRAY_HIP(launch_render(k, static_cast<hipStream_t>(stream)));
+    return TRAY_OK;
+}
+
+int tray_render(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,
+                const tray_params* p, int32_t device, void* out, uint32_t* segments_out) {
+    if (!bg || !cam || !out) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+    int rc = validate_params(p);
+    if (rc) return rc;
+    rc = validate_spheres(spheres, n);
+    if (rc) return rc;
+    DeviceState* st = nullptr;
+    rc = device_state(device, &st);
+    if (rc) return rc;
+    const int32_t rows = tray_params_rows(p);
+    const size_t npix = (size_t)rows * (size_t)p->width;
+    if (npix == 0) return TRAY_OK;
+    tray_scene_t sc = nullptr;
+    rc = tray_scene_upload(spheres, n, bg, device, &sc);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(st->mu);
+    auto cleanup = [&](int code) {
+        tray_scene_release(sc);
+        return code;
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess && !st->stream) e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
+    const size_t out_bytes = npix * bytes_per_pixel(p->output);
+    if (e == hipSuccess && st->out_ws_bytes < out_bytes) {
+        if (st->out_ws) (void)hipFree(st->out_ws);
+        st->out_ws = nullptr;
+        st->out_ws_bytes = 0;
+        e = hipMalloc(&st->out_ws, out_bytes);
+        if (e == hipSuccess) st->out_ws_bytes = out_bytes;
+    }
+    const size_t seg_bytes = npix * sizeof(uint32_t);
+    if (e == hipSuccess && segments_out && st->seg_ws_bytes < seg_bytes) {
+        if (st->seg_ws) (void)hipFree(st->seg_ws);
+        st->seg_ws = nullptr;
+        st->seg_ws_bytes = 0;
+        e = hipMalloc(&st->seg_ws, seg_bytes);
+        if (e == hipSuccess) st->seg_ws_bytes = seg_bytes;
+    }
+    if (e != hipSuccess) return cleanup(hip_fail(e, "workspace"));
+    rc = tray_render_async(sc, cam, p, st->out_ws, segments_out ? st->seg_ws : nullptr, st->stream);
+    if (rc) return cleanup(rc);
+    e = hipMemcpyAsync(out, st->out_ws, out_bytes, hipMemcpyDeviceToHost, st->stream);
+    if (e == hipSuccess && segments_out)
+        e = hipMemcpyAsync(segments_out, st->seg_ws, seg_bytes, hipMemcpyDeviceToHost, st->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(st->stream);
+    if (e != hipSuccess) return cleanup(hip_fail(e, "render"));
+    return cleanup(TRAY_OK);
+}
+
+int tray_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_devices_mu);
+    for (size_t d = 0; d < g_devices.size(); ++d) {
+        DeviceState* st = g_devices[d];
+        if (!st) continue;
+        std::lock_guard<std::mutex> lk2(st->mu);
+        (void)hipSetDevice((int)d);
+        if (st->out_ws) (void)hipFree(st->out_ws);
+        if (st->seg_ws) (void)hipFree(st->seg_ws);
+        if (st->stream) (void)hipStreamDestroy(st->stream);
+        st->out_ws = nullptr;
+        st->seg_ws = nullptr;
+        st->stream = nullptr;
+        st->out_ws_bytes = st->seg_ws_bytes = 0;
+    }
+    return TRAY_OK;
+}
+
+#pragma GCC visibility pop
+}  // extern "C"

@@ -1,0 +1,60 @@
+// Internal launch interface between the C-ABI glue (tray_abi.hip) and the
+// megakernel (tray_kernel.hip). Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace tray {
+
+enum : int32_t { kLambertian = 1, kMetal = 2, kDielectric = 3 };
+enum : int32_t { kOutRGBF64 = 0, kOutRGBF32 = 1, kOutRGBA8 = 2 };
+
+// Sphere geometry is staged into LDS as double4 {cx, cy, cz, R*R} (32 B).
+// Up to 160 KiB of LDS per workgroup on gfx950 -> 5120 spheres; larger scenes
+// read the same array from global memory (L2/L1-resident).
+constexpr size_t kMaxLDSBytes = 160 * 1024;
+
+// Per-sphere shading record, read only for the closest hit (48 B).
+struct MatRec {
+    double albedo[3];
+    double param;   // Metal.Fuzz / Dielectric.RefIdx
+    double radius;  // Sphere.Radius (normal = (P - C) / R, ray/objects.go:100)
+    int32_t type;
+    int32_t pad;
+};
+
+struct CamRec {
+    double position[3];
+    double pixel00[3];
+    double pixel_x[3];
+    double pixel_y[3];
+    double defocus_u[3];
+    double defocus_v[3];
+    double aperture;
+};
+
+struct V3 {
+    double x, y, z;
+};
+
+struct KernelParams {
+    const double4* geo;
+    const MatRec* mat;
+    int32_t n;
+    int32_t width, height, spp, max_depth;
+    int32_t y_start, rows, tile_rows, tile_count, tile_index;
+    int32_t out_format;
+    double ray_radius;
+    double focus_time;  // FocusDistance / FocalLength (ray/camera.go:134)
+    uint64_t seed;
+    CamRec cam;
+    V3 bg_a, bg_b;
+    void* out;
+    uint32_t* segments;
+};
+
+hipError_t launch_render(const KernelParams& p, hipStream_t stream);
+
+}  // namespace tray
