@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of libtray_amd.so builds in ONE process (same device,
+same data): per round every variant renders the frame once; reports the median
+and min kernel time per variant (HIP events on the launch stream).
+
+    python tools/ab_bench.py [--config c2] [--rounds 5] NAME=path/libtray_amd.so ...
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("variants", nargs="+")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from bench import CONFIGS
+    from tray_amd import _lib, ray
+
+    label, seed, half, W, H, spp, depth = CONFIGS[args.config]
+    spheres = ray.rich_scene_array(seed, half)
+    cam = ray.RichSceneCamera()
+    cam.Initialize(W, H)
+    bg = ray._background(ray.DefaultBackground())
+    params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
+    stream = torch.cuda.current_stream()
+    runs = {}
+    for v in args.variants:
+        name, path = v.split("=", 1)
+        path = os.path.abspath(path)
+        runs[name] = dict(scene=_lib.DeviceScene(spheres, bg, 0, path),
+                          out=torch.empty((H, W, 3), dtype=torch.float32, device="cuda"), ms=[])
+    ref = None
+    for r in range(args.rounds + 1):
+        for name, st in runs.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            st["scene"].render_async(cam._state, params, st["out"].data_ptr(), None, stream.cuda_stream)
+            b.record(stream)
+            torch.cuda.synchronize()
+            if r > 0:
+                st["ms"].append(a.elapsed_time(b))
+            if ref is None:
+                ref = st["out"].clone()
+            elif r == 0:
+                st["equal_to_first"] = bool(torch.equal(ref, st["out"]))
+    samples = W * H * spp
+    for name, st in runs.items():
+        med = float(np.median(st["ms"]))
+        print(json.dumps({"variant": name, "median_ms": round(med, 3), "min_ms": round(min(st["ms"]), 3),
+                          "mrays": round(samples / med / 1e3, 1), "equal_to_first": st.get("equal_to_first", True)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Counter passes for the render kernel (run on the GPU box from the repo root).
+# Each --pmc pass is its own rocprofv3 run (never combined with tracing domains).
+#   usage: tools/profile_counters.sh <outdir> [bench.py args...]
+set -u
+OUT=${1:-gpurun_out/pmc}; shift || true
+ARGS=${*:-"--steps 1 --warmup 0 --no-cpu-baseline"}
+export TMPDIR=/tmp
+mkdir -p "$OUT"
+i=0
+for SET in \
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU" \
+  "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_INT32" \
+  "GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_INT64 SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VALU_FLOPS_FP64" ; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex render_kernel -d "$OUT/p$i" -o pmc \
+      --output-format csv -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
+  echo "pass $i rc=$?" >> "$OUT/status.txt"
+done

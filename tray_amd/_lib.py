@@ -121,19 +121,21 @@ EXPORTS = (
     "tray_to_srgba",
 )
 
-_lib = None
+_libs: dict = {}
 
 
-def lib() -> ctypes.CDLL:
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def lib(path: str | None = None) -> ctypes.CDLL:
+    """The C-ABI library (default: the in-tree build). `path` loads another build
+    of the same ABI (used by tools/ab_bench.py to compare kernel variants)."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: the HIP renderer is not built. Run `make -C tray_amd` "
+            f"{path} is missing: the HIP renderer is not built. Run `make -C tray_amd` "
             "(or __graft_entry__.build()). There is no CPU fallback."
         )
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, i32, u32p = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32)
     L.tray_abi_version.restype = i32
     L.tray_last_error.restype = ctypes.c_char_p
@@ -153,7 +155,7 @@ def lib() -> ctypes.CDLL:
     L.tray_params_rows.argtypes = [ctypes.POINTER(Params)]
     L.tray_params_rows.restype = i32
     L.tray_to_srgba.argtypes = [vp, ctypes.c_size_t, vp]
-    _lib = L
+    _libs[path] = L
     return L
 
 
@@ -204,25 +206,31 @@ def render(spheres, background: Background, camera: CameraState, params: Params,
 
 
 class DeviceScene:
-    """A scene uploaded once to one device (tray_scene_upload); render many times."""
+    """A scene uploaded once to one device (tray_scene_upload); render many times.
+    Renders of one DeviceScene must be ordered on one stream (shared work queue)."""
 
-    def __init__(self, spheres, background: Background, device: int = 0):
+    def __init__(self, spheres, background: Background, device: int = 0, lib_path: str | None = None):
+        self.L = lib(lib_path)
         s = spheres_array(spheres)
         h = ctypes.c_void_p()
-        check(lib().tray_scene_upload(s.ctypes.data if len(s) else None, len(s), ctypes.byref(background), device,
-                                      ctypes.byref(h)))
+        rc = self.L.tray_scene_upload(s.ctypes.data if len(s) else None, len(s), ctypes.byref(background), device,
+                                      ctypes.byref(h))
+        if rc != TRAY_OK:
+            raise TrayError(rc, self.L.tray_last_error().decode())
         self.handle = h
         self.device = device
         self.n = len(s)
 
     def render_async(self, camera: CameraState, params: Params, out_ptr: int, segments_ptr: int | None = None,
                      stream: int | None = None) -> None:
-        check(lib().tray_render_async(self.handle, ctypes.byref(camera), ctypes.byref(params), out_ptr,
-                                      segments_ptr, stream))
+        rc = self.L.tray_render_async(self.handle, ctypes.byref(camera), ctypes.byref(params), out_ptr, segments_ptr,
+                                      stream)
+        if rc != TRAY_OK:
+            raise TrayError(rc, self.L.tray_last_error().decode())
 
     def release(self) -> None:
         if self.handle:
-            lib().tray_scene_release(self.handle)
+            self.L.tray_scene_release(self.handle)
             self.handle = ctypes.c_void_p()
 
     def __del__(self):

@@ -86,11 +86,16 @@ static int device_state(int32_t device, DeviceState** out) {
 
 }  // namespace tray
 
+// A scene resident on one device. Renders of one scene handle share its work
+// queue counter, so they must be ordered on one stream (the queue is re-zeroed
+// by every launch).
 struct tray_scene_s {
     int32_t device;
     int32_t n;
-    double4* geo;
+    int32_t n_pad;
+    double4* geo;  // n_pad entries, NaN-padded (see tray::KernelParams::geo)
     tray::MatRec* mat;
+    uint32_t* queue;
     tray::V3 bg_a, bg_b;
 };
 
@@ -174,7 +179,9 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     rc = device_state(device, &st);
     if (rc) return rc;
     TRAY_HIP(hipSetDevice(device));
-    std::vector<double4> geo((size_t)n);
+    const int32_t n_pad = padded_spheres(n);
+    const double qnan = std::nan("");
+    std::vector<double4> geo((size_t)n_pad, make_double4(qnan, qnan, qnan, qnan));
     std::vector<MatRec> mat((size_t)n);
     for (int32_t i = 0; i < n; ++i) {
         const tray_sphere& s = spheres[i];
@@ -192,21 +199,23 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     tray_scene_s* sc = new tray_scene_s();
     sc->device = device;
     sc->n = n;
+    sc->n_pad = n_pad;
     sc->geo = nullptr;
     sc->mat = nullptr;
+    sc->queue = nullptr;
     sc->bg_a = V3{bg->color_a[0], bg->color_a[1], bg->color_a[2]};
     sc->bg_b = V3{bg->color_b[0], bg->color_b[1], bg->color_b[2]};
-    if (n > 0) {
-        hipError_t e = hipMalloc(&sc->geo, sizeof(double4) * (size_t)n);
-        if (e == hipSuccess) e = hipMalloc(&sc->mat, sizeof(MatRec) * (size_t)n);
-        if (e == hipSuccess) e = hipMemcpy(sc->geo, geo.data(), sizeof(double4) * (size_t)n, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            (void)hipFree(sc->geo);
-            (void)hipFree(sc->mat);
-            delete sc;
-            return hip_fail(e, "scene upload");
-        }
+    hipError_t e = hipMalloc(&sc->geo, sizeof(double4) * (size_t)n_pad);
+    if (e == hipSuccess) e = hipMalloc(&sc->queue, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpy(sc->geo, geo.data(), sizeof(double4) * (size_t)n_pad, hipMemcpyHostToDevice);
+    if (e == hipSuccess && n > 0) e = hipMalloc(&sc->mat, sizeof(MatRec) * (size_t)n);
+    if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(sc->geo);
+        (void)hipFree(sc->mat);
+        (void)hipFree(sc->queue);
+        delete sc;
+        return hip_fail(e, "scene upload");
     }
     *out = sc;
     return TRAY_OK;
@@ -217,6 +226,7 @@ int tray_scene_release(tray_scene_t sc) {
     (void)hipSetDevice(sc->device);
     if (sc->geo) (void)hipFree(sc->geo);
     if (sc->mat) (void)hipFree(sc->mat);
+    if (sc->queue) (void)hipFree(sc->queue);
     delete sc;
     return TRAY_OK;
 }
@@ -231,6 +241,8 @@ int tray_render_async(tray_scene_t sc, const tray_camera* cam, const tray_params
     k.geo = sc->geo;
     k.mat = sc->mat;
     k.n = sc->n;
+    k.n_pad = sc->n_pad;
+    k.queue = sc->queue;
     k.width = p->width;
     k.height = p->height;
     k.spp = p->rays_per_pixel;

@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "rng.hpp"
 #include "tray_kernel.hpp"
 
@@ -155,137 +157,27 @@ __device__ __forceinline__ int32_t row_of(const KernelParams& p, int32_t j) {
     return p.y_start + (t * p.tile_count + p.tile_index) * p.tile_rows + within;
 }
 
-template <bool kLDS>
-__global__ __launch_bounds__(256) void render_kernel(KernelParams p) {
-    extern __shared__ __attribute__((aligned(16))) double4 s_geo[];
-    const double4* __restrict__ geo = p.geo;
-    if constexpr (kLDS) {
-        for (int i = threadIdx.x; i < p.n; i += blockDim.x) s_geo[i] = p.geo[i];
-        __syncthreads();
-        geo = s_geo;
-    }
+// Per-lane path state. A lane owns one pixel at a time and walks its samples
+// in order; when the last sample ends it writes the pixel and takes another.
+struct Lane {
+    D3 org, dir, thr, sum;
+    uint32_t pixel, sample, bounce, segments;
+    int32_t x, j;  // image column, compact output row
+    double fx, fy;
+    bool busy;
+};
 
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int j = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool valid = x < p.width && j < p.rows;
-    const int32_t y = valid ? row_of(p, j) : 0;
-    const uint32_t pixel = (uint32_t)y * (uint32_t)p.width + (uint32_t)x;
-    const double fx = (double)x, fy = (double)y;
-
-    D3 org = d3(0, 0, 0), dir = d3(0, 0, 1);
-    D3 thr = d3(1, 1, 1);
-    D3 sum = d3(0, 0, 0);
-    uint32_t sample = 0, bounce = 0, segments = 0;
-    bool done = !valid;
-    if (!done) get_ray(p, pixel, 0u, fx, fy, org, dir);
-
-    const int n = p.n;
-    while (__ballot(!done) != 0ull) {
-        if (!done) {
-            ++segments;
-            // Scene.Hit over every sphere in list order; a = |D|^2 hoisted (same bits).
-            const double a = length_sq(dir);
-            double closest = __builtin_inf();
-            int best = -1;
-            for (int i = 0; i < n; ++i) {
-                const double4 g = geo[i];
-                const double ocx = g.x - org.x;
-                const double ocy = g.y - org.y;
-                const double ocz = g.z - org.z;
-                const double h = dir.x * ocx + dir.y * ocy + dir.z * ocz;
-                const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - g.w;
-                const double disc = h * h - a * c;
-                if (disc >= 0) {
-                    const double sq = __builtin_sqrt(disc);
-                    double root = (h - sq) / a;
-                    if (!(root > 1e-6 && root < closest)) {
-                        root = (h + sq) / a;
-                        if (!(root > 1e-6 && root < closest)) continue;
-                    }
-                    closest = root;
-                    best = i;
-                }
-            }
-
-            bool path_end = false;
-            D3 color = d3(0, 0, 0);
-            if (best >= 0) {
-                const double4 g = geo[best];
-                const MatRec m = p.mat[best];
-                const D3 center = d3(g.x, g.y, g.z);
-                const D3 point = add(org, smul(dir, closest));
-                const D3 outward = sdiv(sub(point, center), m.radius);
-                const bool front = dot(dir, outward) < 0;
-                const D3 normal = front ? outward : neg(outward);
-                const D3 albedo = d3(m.albedo[0], m.albedo[1], m.albedo[2]);
-                bool scattered = true;
-                D3 new_dir;
-                D3 att = albedo;
-                if (m.type == kLambertian) {
-                    new_dir = add(normal, unit_vector(p.seed, pixel, sample, bounce));
-                    if (near_zero(new_dir)) new_dir = normal;
-                } else if (m.type == kMetal) {
-                    D3 reflected = reflect(unit(dir), normal);
-                    if (m.param > 0.0) reflected = add(reflected, smul(unit_vector(p.seed, pixel, sample, bounce), m.param));
-                    new_dir = reflected;
-                    scattered = dot(new_dir, normal) > 0;
-                } else {  // kDielectric
-                    att = d3(1.0, 1.0, 1.0);
-                    const double ratio = front ? 1.0 / m.param : m.param;
-                    const D3 ud = unit(dir);
-                    const double cos_theta = go_min(dot(neg(ud), normal), 1.0);
-                    const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
-                    const bool cannot_refract = ratio * sin_theta > 1.0;
-                    bool do_reflect = cannot_refract;
-                    if (!do_reflect) {
-                        const U2 u = philox_uniforms(p.seed, pixel, sample, bounce, kPurposeScatter << 24);
-                        do_reflect = reflectance(cos_theta, ratio) > u.u0;
-                    }
-                    new_dir = do_reflect ? reflect(ud, normal) : refract(ud, normal, ratio);
-                }
-                if (scattered) {
-                    thr = mul(thr, att);
-                    org = point;
-                    dir = new_dir;
-                    ++bounce;
-                    path_end = bounce >= (uint32_t)p.max_depth;  // RayColor(depth 0) -> black
-                } else {
-                    path_end = true;  // absorbed -> black
-                }
-            } else {
-                // AmbientLight.Hit (ray/objects.go:68-73)
-                const D3 u = unit(dir);
-                const double t = 0.5 * (u.y + 1.0);
-                const D3 sky = add(smul(d3(p.bg_a.x, p.bg_a.y, p.bg_a.z), 1.0 - t), smul(d3(p.bg_b.x, p.bg_b.y, p.bg_b.z), t));
-                color = mul(thr, sky);
-                path_end = true;
-            }
-            if (path_end) {
-                sum = add(sum, color);
-                ++sample;
-                if (sample >= (uint32_t)p.spp) {
-                    done = true;
-                } else {
-                    thr = d3(1, 1, 1);
-                    bounce = 0;
-                    get_ray(p, pixel, sample, fx, fy, org, dir);
-                }
-            }
-        }
-    }
-
-    if (!valid) return;
+template <int kFmt>
+__device__ __forceinline__ void write_pixel(const KernelParams& p, const Lane& L) {
     const double inv = 1.0 / (double)p.spp;  // colorSumDiv (ray/tracer.go:123)
-    const D3 mean = smul(sum, inv);
-    const size_t off = (size_t)j * (size_t)p.width + (size_t)x;
-    if (p.out_format == kOutRGBF64) {
+    const D3 mean = smul(L.sum, inv);
+    const size_t off = (size_t)L.j * (size_t)p.width + (size_t)L.x;
+    if constexpr (kFmt == kOutRGBF64) {
         double* o = static_cast<double*>(p.out) + off * 3;
         o[0] = mean.x;
         o[1] = mean.y;
         o[2] = mean.z;
-    } else if (p.out_format == kOutRGBF32) {
+    } else if constexpr (kFmt == kOutRGBF32) {
         float* o = static_cast<float*>(p.out) + off * 3;
         o[0] = (float)mean.x;
         o[1] = (float)mean.y;
@@ -295,28 +187,326 @@ __global__ __launch_bounds__(256) void render_kernel(KernelParams p) {
                               (linear_to_srgb(mean.z) << 16) | (255u << 24);
         static_cast<uint32_t*>(p.out)[off] = rgba;
     }
-    if (p.segments) p.segments[off] = segments;
+    if (p.segments) p.segments[off] = L.segments;
 }
 
-hipError_t launch_render(const KernelParams& p, hipStream_t stream) {
-    const dim3 block(256);
-    const dim3 grid((unsigned)((p.width + 15) / 16), (unsigned)((p.rows + 15) / 16));
-    const size_t lds = (size_t)p.n * sizeof(double4);
-    if (p.rows <= 0) return hipSuccess;
-    if (lds <= kMaxLDSBytes) {
-        static bool attr_set[64] = {};
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (dev >= 0 && dev < 64 && !attr_set[dev]) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&render_kernel<true>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLDSBytes);
-            if (e != hipSuccess) return e;
-            attr_set[dev] = true;
+// Candidate root of one sphere whose discriminant is >= 0 (Sphere.Hit,
+// ray/objects.go:86-94): the first root inside (1e-6, closest) wins.
+__device__ __forceinline__ void candidate(double h, double disc, double a, int idx, double& closest, int& best) {
+    if (disc >= 0) {
+        const double sq = __builtin_sqrt(disc);
+        double root = (h - sq) / a;
+        bool ok = root > 1e-6 && root < closest;
+        if (!ok) {
+            root = (h + sq) / a;
+            ok = root > 1e-6 && root < closest;
         }
-        hipLaunchKernelGGL(render_kernel<true>, grid, block, lds, stream, p);
-    } else {
-        hipLaunchKernelGGL(render_kernel<false>, grid, block, 0, stream, p);
+        if (ok) {
+            closest = root;
+            best = idx;
+        }
     }
+}
+
+// 17 FP64 add/mul per sphere, op order of Sphere.Hit (ray/objects.go:82-86).
+__device__ __forceinline__ void quad(const double4 g, const D3& org, const D3& dir, double a, double& h,
+                                     double& disc) {
+    const double ocx = g.x - org.x;
+    const double ocy = g.y - org.y;
+    const double ocz = g.z - org.z;
+    h = dir.x * ocx + dir.y * ocy + dir.z * ocz;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - g.w;
+    disc = h * h - a * c;
+}
+
+#ifndef TRAY_UNROLL
+#define TRAY_UNROLL 8
+#endif
+#ifndef TRAY_PREFETCH
+#define TRAY_PREFETCH 0
+#endif
+
+// Scene.Hit (ray/objects.go:37-46) over geometry padded with NaN spheres (a
+// NaN discriminant is never >= 0). Spheres are tested in groups of U that
+// share one wave-level branch into the (rare) sqrt/div path; inside a group
+// they are visited in list order, so the closest root with the lowest index
+// wins exactly as in the reference's linear scan. With PF the next group is
+// loaded while the current one computes (the padding keeps that in bounds).
+template <int U, bool PF, typename GeoPtr>
+__device__ __forceinline__ int scene_hit(GeoPtr geo, int n, const D3& org, const D3& dir, double& closest) {
+    const double a = length_sq(dir);  // hoisted: same bits as per sphere
+    closest = __builtin_inf();
+    int best = -1;
+    const int ngroups = (n + U - 1) / U;
+    double4 nx[U];
+    if constexpr (PF) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) nx[k] = geo[k];
+    }
+    for (int gi = 0; gi < ngroups; ++gi) {
+        const int i = gi * U;
+        double4 g[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if constexpr (PF) {
+                g[k] = nx[k];
+                nx[k] = geo[i + U + k];
+            } else {
+                g[k] = geo[i + k];
+            }
+        }
+        double h[U], d[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) quad(g[k], org, dir, a, h[k], d[k]);
+        double m = d[0];
+#pragma unroll
+        for (int k = 1; k < U; ++k) m = __builtin_fmax(m, d[k]);  // maxNum drops NaN padding
+        if (m >= 0) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) candidate(h[k], d[k], a, i + k, closest, best);
+        }
+    }
+    return best;
+}
+
+// Where the sphere loop reads geometry from: 0 = LDS (staged once per
+// workgroup, broadcast ds_read_b128), 1 = scalar loads through the constant
+// address space (the index is wave-uniform, so the data lands in SGPRs and
+// costs neither LDS bandwidth nor VGPRs).
+#ifndef TRAY_GEO
+#define TRAY_GEO 0
+#endif
+typedef const __attribute__((address_space(4))) double* ConstD;
+
+// Geometry accessors: element i = {cx, cy, cz, R*R}.
+struct GeoVec {
+    const double4* __restrict__ p;
+    __device__ __forceinline__ double4 operator[](int i) const { return p[i]; }
+};
+struct GeoScalar {
+    ConstD p;
+    __device__ __forceinline__ double4 operator[](int i) const {
+        return make_double4(p[4 * i], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]);
+    }
+};
+
+// One Scene.Hit + shading step of the lane's current path (one recursion level
+// of RayColor, ray/objects.go:49-62). Returns true when the path ended.
+template <typename GeoPtr>
+__device__ __forceinline__ bool segment(const KernelParams& p, GeoPtr geo, Lane& L, D3& color) {
+    ++L.segments;
+    double closest;
+    const int best = scene_hit<TRAY_UNROLL, TRAY_PREFETCH != 0>(geo, p.n, L.org, L.dir, closest);
+    if (best < 0) {
+        // AmbientLight.Hit (ray/objects.go:68-73)
+        const D3 u = unit(L.dir);
+        const double t = 0.5 * (u.y + 1.0);
+        const D3 sky = add(smul(d3(p.bg_a.x, p.bg_a.y, p.bg_a.z), 1.0 - t), smul(d3(p.bg_b.x, p.bg_b.y, p.bg_b.z), t));
+        color = mul(L.thr, sky);
+        return true;
+    }
+    const double4 g = geo[best];
+    const MatRec m = p.mat[best];
+    const D3 point = add(L.org, smul(L.dir, closest));                 // Ray.At (ray/ray.go:23-25)
+    const D3 outward = sdiv(sub(point, d3(g.x, g.y, g.z)), m.radius);  // ray/objects.go:100
+    const bool front = dot(L.dir, outward) < 0;                        // SetFaceNormal (:19-26)
+    const D3 normal = front ? outward : neg(outward);
+    bool scattered = true;
+    D3 new_dir;
+    D3 att = d3(m.albedo[0], m.albedo[1], m.albedo[2]);
+    if (m.type == kLambertian) {  // ray/materials.go:13-20
+        new_dir = add(normal, unit_vector(p.seed, L.pixel, L.sample, L.bounce));
+        if (near_zero(new_dir)) new_dir = normal;
+    } else if (m.type == kMetal) {  // ray/materials.go:28-37
+        D3 reflected = reflect(unit(L.dir), normal);
+        if (m.param > 0.0)
+            reflected = add(reflected, smul(unit_vector(p.seed, L.pixel, L.sample, L.bounce), m.param));
+        new_dir = reflected;
+        scattered = dot(new_dir, normal) > 0;
+    } else {  // Dielectric, ray/materials.go:44-64
+        att = d3(1.0, 1.0, 1.0);
+        const double ratio = front ? 1.0 / m.param : m.param;
+        const D3 ud = unit(L.dir);
+        const double cos_theta = go_min(dot(neg(ud), normal), 1.0);
+        const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
+        bool do_reflect = ratio * sin_theta > 1.0;  // cannot refract
+        if (!do_reflect) {
+            const U2 u = philox_uniforms(p.seed, L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
+            do_reflect = reflectance(cos_theta, ratio) > u.u0;
+        }
+        new_dir = do_reflect ? reflect(ud, normal) : refract(ud, normal, ratio);
+    }
+    color = d3(0, 0, 0);
+    if (!scattered) return true;  // absorbed -> black
+    L.thr = mul(L.thr, att);
+    L.org = point;
+    L.dir = new_dir;
+    ++L.bounce;
+    return L.bounce >= (uint32_t)p.max_depth;  // RayColor(depth 0) -> black
+}
+
+// Work item w (64 pixels = one 8x8 tile of the compact row space) -> pixel.
+__device__ __forceinline__ bool decode_pixel(const KernelParams& p, uint32_t item, int32_t& x, int32_t& j) {
+    const uint32_t tile = item >> 6, r = item & 63u;
+    const uint32_t tx = tile % (uint32_t)p.tiles_x, ty = tile / (uint32_t)p.tiles_x;
+    x = (int32_t)(tx * 8u + (r & 7u));
+    j = (int32_t)(ty * 8u + (r >> 3));
+    return x < p.width && j < p.rows;
+}
+
+__device__ __forceinline__ void start_pixel(const KernelParams& p, Lane& L, int32_t x, int32_t j) {
+    const int32_t y = row_of(p, j);
+    L.x = x;
+    L.j = j;
+    L.pixel = (uint32_t)y * (uint32_t)p.width + (uint32_t)x;  // global index: tiling-independent RNG key
+    L.fx = (double)x;
+    L.fy = (double)y;
+    L.sample = 0;
+    L.bounce = 0;
+    L.segments = 0;
+    L.thr = d3(1, 1, 1);
+    L.sum = d3(0, 0, 0);
+    L.busy = true;
+    get_ray(p, L.pixel, 0u, L.fx, L.fy, L.org, L.dir);
+}
+
+// Persistent megakernel: waves pull 64-pixel work items from a global counter
+// and lanes refill individually, so no lane idles while the frame has work.
+template <bool kLDS, int kFmt>
+#ifndef TRAY_WAVES_PER_SIMD
+#define TRAY_WAVES_PER_SIMD 5
+#endif
+__global__ __launch_bounds__(256, TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
+    extern __shared__ __attribute__((aligned(16))) double4 s_geo[];
+#if TRAY_GEO == 1
+    const GeoScalar geo{(ConstD)(const double*)p.geo};
+#else
+    GeoVec geo{p.geo};
+    if constexpr (kLDS) {
+        for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) s_geo[i] = p.geo[i];
+        __syncthreads();
+        geo.p = s_geo;
+    }
+#endif
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    Lane L;
+    L.busy = false;
+    uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
+    bool exhausted = false;
+
+    while (true) {
+        // Refill idle lanes from the wave's pool, fetching 64-item chunks from the global queue.
+        uint64_t idle = __ballot(!L.busy);
+        while (idle != 0ull && !exhausted) {
+            if (pool_next == pool_end) {
+                uint32_t c = 0;
+                if (lane == 0) c = atomicAdd(p.queue, 1u);
+                c = __shfl(c, 0);
+                if (c >= p.nchunks) {
+                    exhausted = true;
+                    break;
+                }
+                pool_next = c * 64u;
+                pool_end = pool_next + 64u;
+            }
+            const uint32_t n_idle = (uint32_t)__popcll(idle);
+            const uint32_t take = min(n_idle, pool_end - pool_next);
+            if (!L.busy) {
+                const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+                if (rank < take) {
+                    int32_t x, j;
+                    if (decode_pixel(p, pool_next + rank, x, j)) start_pixel(p, L, x, j);
+                }
+            }
+            pool_next += take;
+            idle = __ballot(!L.busy);
+        }
+        if (__ballot(L.busy) == 0ull) break;
+        if (L.busy) {
+            D3 color;
+            if (segment(p, geo, L, color)) {
+                L.sum = add(L.sum, color);  // Add(colorSum, color) (ray/tracer.go:143)
+                ++L.sample;
+                if (L.sample >= (uint32_t)p.spp) {
+                    write_pixel<kFmt>(p, L);
+                    L.busy = false;
+                } else {
+                    L.thr = d3(1, 1, 1);
+                    L.bounce = 0;
+                    get_ray(p, L.pixel, L.sample, L.fx, L.fy, L.org, L.dir);
+                }
+            }
+        }
+    }
+}
+
+using KernelFn = void (*)(KernelParams);
+
+static KernelFn pick_kernel(bool use_lds, int fmt) {
+    if (use_lds) {
+        if (fmt == kOutRGBF64) return render_kernel<true, kOutRGBF64>;
+        if (fmt == kOutRGBF32) return render_kernel<true, kOutRGBF32>;
+        return render_kernel<true, kOutRGBA8>;
+    }
+    if (fmt == kOutRGBF64) return render_kernel<false, kOutRGBF64>;
+    if (fmt == kOutRGBF32) return render_kernel<false, kOutRGBF32>;
+    return render_kernel<false, kOutRGBA8>;
+}
+
+// Blocks the device keeps resident for this kernel and LDS size (persistent grid cap).
+static int resident_blocks(int device, KernelFn fn, size_t lds) {
+    hipDeviceProp_t prop;
+    int cus = 256;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), 256, lds) !=
+            hipSuccess ||
+        per_cu <= 0)
+        per_cu = 2;
+    return cus * per_cu;
+}
+
+hipError_t launch_render(KernelParams p, hipStream_t stream) {
+    if (p.rows <= 0) return hipSuccess;
+    p.tiles_x = (p.width + 7) / 8;
+    const uint32_t tiles_y = (uint32_t)((p.rows + 7) / 8);
+    p.nchunks = (uint32_t)p.tiles_x * tiles_y;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const size_t lds_bytes = (size_t)p.n_pad * sizeof(double4);
+    const bool use_lds = TRAY_GEO == 0 && lds_bytes <= kMaxLDSBytes;
+    const size_t lds = use_lds ? lds_bytes : 0;
+    const KernelFn fn = pick_kernel(use_lds, p.out_format);
+    // Per-device, per-(kernel, LDS size) launch setup, cached.
+    struct Setup {
+        int dev;
+        KernelFn fn;
+        size_t lds;
+        int blocks;
+    };
+    static thread_local Setup cache[8] = {};
+    static thread_local int cache_next = 0;
+    int blocks = 0;
+    for (const Setup& c : cache)
+        if (c.fn == fn && c.dev == dev && c.lds == lds && c.blocks > 0) blocks = c.blocks;
+    if (blocks == 0) {
+        if (use_lds) {
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kMaxLDSBytes);
+            if (e != hipSuccess) return e;
+        }
+        blocks = resident_blocks(dev, fn, lds);
+        cache[cache_next] = Setup{dev, fn, lds, blocks};
+        cache_next = (cache_next + 1) % 8;
+    }
+    // Enough waves for every item, capped at what the device keeps resident.
+    const uint32_t want = (p.nchunks + 3u) / 4u;
+    const uint32_t grid = std::min<uint32_t>(want, (uint32_t)blocks);
+    e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, stream, p);
     return hipGetLastError();
 }
 

@@ -40,9 +40,13 @@ struct V3 {
 };
 
 struct KernelParams {
-    const double4* geo;
+    const double4* geo;  // n_pad entries: n spheres, then NaN padding (never hit)
     const MatRec* mat;
+    uint32_t* queue;     // work-item counter, zeroed before every launch
     int32_t n;
+    int32_t n_pad;       // round_up(n, 4) + 4
+    int32_t tiles_x;     // 8x8 pixel tiles per compact row band
+    uint32_t nchunks;    // 64-pixel work items
     int32_t width, height, spp, max_depth;
     int32_t y_start, rows, tile_rows, tile_count, tile_index;
     int32_t out_format;
@@ -55,6 +59,9 @@ struct KernelParams {
     uint32_t* segments;
 };
 
-hipError_t launch_render(const KernelParams& p, hipStream_t stream);
+hipError_t launch_render(KernelParams p, hipStream_t stream);
+
+// Padded geometry length for n spheres (see KernelParams::geo).
+inline int32_t padded_spheres(int32_t n) { return ((n + 3) / 4) * 4 + 4; }
 
 }  // namespace tray
