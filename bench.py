@@ -12,12 +12,15 @@ ends with ONE RCCL gather of the row tiles to rank 0 ("scaling": "strong": the
 frame is fixed as N grows). value = W*H*r*steps / max-over-ranks wall time.
 
 Also reported (rank 0):
-  roofline     the megakernel against the FP64 VALU roof (it is compute bound;
-               HBM traffic is ~1e-5 of the roof and reported under "hbm"):
-               achieved = algorithmic FP64 ops per launch / mean kernel time,
-               ops = 17*N_spheres*segments + 60*segments + 40*samples
-               (SURVEY.md §8(d)); segments are counted by the kernel itself in
-               an untimed launch (bit-exact with the oracle, tests/).
+  roofline     the megakernel against the VALU roof (it is compute bound; HBM
+               traffic is ~1e-5 of the roof and reported under "hbm"):
+               achieved = algorithmic VALU work per launch / mean kernel time,
+               in FP64-instruction equivalents: FP64 ops = 17 per ray-sphere
+               test + 60 per segment + 40 per sample; FP32
+               ops = 19 per ray-box test of the exact-culling BVH, counted at
+               half weight (FP32 issues at 2x the FP64 rate). Tests, segments
+               and box tests are counted by the kernel itself in an untimed
+               instrumented launch (segments are bit-exact with the oracle).
   cpu_baseline the oracle (C port of the reference's CPU loop with the
                reference's chunk-queue scheduler, ray/tracer.go:86-116) timed on
                a bounded row sample of the same frame on the host cores.
@@ -59,6 +62,7 @@ def main() -> int:
     ap.add_argument("--tile-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-step", type=int, default=12, help="oracle renders every k-th row of the frame")
+    ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")
     args = ap.parse_args()
 
     import torch
@@ -83,7 +87,8 @@ def main() -> int:
     cam.Initialize(W, H)
     bg = ray._background(ray.DefaultBackground())
     scene = _lib.DeviceScene(spheres, bg, local_rank)
-    params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
+    params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32,
+                              flags=_lib.FLAG_LINEAR_SCAN if args.linear else 0)
     params = shard.shard_params(params, args.tile_rows, world, rank)
     rows = _lib.params_rows(params)
     out = torch.empty((rows, W, 3), dtype=torch.float32, device="cuda")
@@ -97,12 +102,11 @@ def main() -> int:
         if world > 1:
             shard.gather_image(out, H, args.tile_rows, world, rank)
 
-    # Untimed: per-pixel Scene.Hit counts for the roofline's algorithmic op count.
-    seg = torch.zeros((rows, W), dtype=torch.int32, device="cuda")
-    render(seg.data_ptr())
+    # Untimed instrumented launch: segments, ray-sphere and ray-box tests for the roofline.
+    stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+    scene.render_stats_async(cam._state, params, out.data_ptr(), stats.data_ptr(), stream.cuda_stream)
     torch.cuda.synchronize()
-    segments_local = int(seg.to(torch.int64).sum().item())
-    del seg
+    segments_local, sphere_tests, box_tests = (int(v) for v in stats.tolist())
 
     for _ in range(args.warmup):
         step()
@@ -146,6 +150,7 @@ def main() -> int:
         "data": "synthetic: RichScene book-cover generator on the counter RNG (include/tray.h), RichSceneCamera",
         "config": {
             "workload": label,
+            "traversal": "linear" if args.linear else "bvh",
             "width": W, "height": H, "rays_per_pixel": spp, "max_depth": depth, "scene_seed": seed,
             "spheres": int(len(spheres)), "output": "float3 f32 linear", "parallelism": f"row-tiles x{world}",
             "tile_rows": args.tile_rows if world > 1 else 0,
@@ -153,7 +158,9 @@ def main() -> int:
     }
     if rank == 0:
         local_samples = rows * W * spp
-        ops = 17.0 * len(spheres) * segments_local + 60.0 * segments_local + 40.0 * local_samples
+        ops64 = 17.0 * sphere_tests + 60.0 * segments_local + 40.0 * local_samples
+        ops32 = 19.0 * box_tests
+        ops = ops64 + 0.5 * ops32
         achieved = ops / (kernel_ms * 1e-3) / 1e12
         out_bytes = rows * W * 12 + len(spheres) * (32 + 48)
         traffic = None
@@ -164,7 +171,7 @@ def main() -> int:
             except (OSError, ValueError):
                 traffic = None
         rec["roofline"] = {
-            "bound": "valu_fp64",
+            "bound": "valu",
             "achieved": round(achieved, 3),
             "peak": FP64_PEAK_OPS,
             "unit": "TFLOP/s",
@@ -172,8 +179,13 @@ def main() -> int:
             "traffic": traffic,
             "kernel_ms": round(kernel_ms, 4),
             "segments_per_launch": segments_local,
-            "ops_per_launch": ops,
-            "ops_model": "17*N*segments + 60*segments + 40*samples, no FMA (SURVEY.md 8d)",
+            "sphere_tests_per_launch": sphere_tests,
+            "box_tests_per_launch": box_tests,
+            "fp64_ops_per_launch": ops64,
+            "fp32_ops_per_launch": ops32,
+            "ops_model": "FP64-instruction equivalents: 17/sphere test + 60/segment + 40/sample (FP64, no FMA; "
+                         "SURVEY.md 8d) + 0.5 x 19/box test (FP32); peak = 78.6 TFLOP/s FP64 vector spec / 2",
+            "traversal": "linear scan" if args.linear else "exact-culling BVH",
             "hbm": {"achieved_GBs": round(out_bytes / (kernel_ms * 1e-3) / 1e9, 3), "peak_GBs": HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": out_bytes, "note": "not the bound"},
         }

@@ -136,7 +136,14 @@ typedef struct tray_params {
     int32_t tile_count; /* >= 1 when tile_rows > 0 */
     int32_t tile_index; /* 0 <= tile_index < tile_count */
     int32_t output;     /* tray_output */
+    int32_t flags;      /* TRAY_FLAG_* */
+    int32_t reserved;   /* must be 0 */
 } tray_params;
+
+/* Force the reference-order linear scan over all spheres (Scene.Hit,
+ * ray/objects.go:37-46) instead of the exact-culling BVH. Both give identical
+ * results; the flag exists for verification and A/B timing. */
+#define TRAY_FLAG_LINEAR_SCAN 1
 
 typedef struct tray_scene_s *tray_scene_t;
 
@@ -186,6 +193,13 @@ int tray_scene_release(tray_scene_t scene);
  * params->output format; segments_device nullable. Returns after enqueueing. */
 int tray_render_async(tray_scene_t scene, const tray_camera *camera, const tray_params *params, void *out_device,
                       uint32_t *segments_device, void *stream);
+
+/* tray_render_async with instrumentation, for roofline accounting: writes the
+ * frame as TRAY_OUT_RGB_F32 into out_device (params->output is ignored) and
+ * stats_device[0..2] = total Scene.Hit calls (segments), ray-sphere tests and
+ * ray-box tests performed (summed over lanes). stats_device is zeroed first. */
+int tray_render_stats_async(tray_scene_t scene, const tray_camera *camera, const tray_params *params,
+                            float *out_device, uint64_t *stats_device, void *stream);
 
 /* Rows rendered by *params (size of the compact output in rows). */
 int32_t tray_params_rows(const tray_params *params);

@@ -32,7 +32,7 @@ def bg_struct(L, bg):
     return L.Background(d3(*bg[0:3]), d3(*bg[3:6]))
 
 
-def gpu_render(L, spheres, bg, cam, w, h, spp, depth, radius, seed, **kw):
+def gpu_render(L, spheres, bg, cam, w, h, spp, depth, radius, seed, **kw):  # kw -> make_params
     p = L.make_params(w, h, depth, spp, radius, seed, **kw)
     return L.render(spheres, bg_struct(L, bg), cam, p, 0, segments=True)
 
@@ -175,3 +175,88 @@ def test_config2_full_size_properties(L, O):
     ref, rseg = O.render_pixels(sc, DEFAULT_BG, st.as_array(), 1280, 720, 64, 50, 0.5, 2, xs, ys)
     check(a[ys, xs], sa[ys, xs], ref, rseg)
     assert sa.min() >= 64 and sa.max() <= 64 * 50
+
+
+# ---------------------------------------------------------------- BVH --------
+BVH_CASES = {
+    # name: (scene, setup, w, h, spp, depth, seed)
+    "book_dof": ("rich2", RICH_SETUP, 160, 90, 8, 50, 2),
+    "book_pinhole": ("rich2", np.r_[RICH_SETUP[:12], 0.0], 128, 72, 2, 50, 5),
+    "dense": ("dense7", RICH_SETUP, 96, 54, 4, 50, 7),
+    "default_scene_below_bvh_threshold": ("default", np.array([-2, 2, 1, 0, 0, -1, 0, 0, 0, 20.0, 0, 3.0, 0.1]), 64,
+                                          40, 4, 10, 1),
+    "top_down": ("rich2", np.array([0.5, 30, 0.25, 0, 0, 0, 0, 0, 1, 40.0, 10.0, 30.0, 0.0]), 96, 96, 4, 50, 3),
+    "inside_big_glass": ("rich2", np.array([0.05, 1.1, 0.02, 4, 1, 0, 0, 1, 0, 70.0, 1.0, 4.0, 0.0]), 64, 48, 4, 50, 4),
+}
+
+
+@pytest.mark.parametrize("case", sorted(BVH_CASES))
+def test_bvh_equals_linear_scan(L, O, case):
+    """The exact-culling BVH must reproduce the reference-order linear scan bit for bit
+    (same closest root, ties to the lowest index) on every pixel."""
+    key, setup, w, h, spp, depth, seed = BVH_CASES[case]
+    sc = scene_for(O, key)
+    st = camera(L, setup, w, h)
+    bvh, sb = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, depth, 0.5, seed)
+    lin, sl = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, depth, 0.5, seed, flags=L.FLAG_LINEAR_SCAN)
+    assert np.array_equal(sb, sl)
+    assert np.array_equal(bvh, lin)
+
+
+def test_bvh_config1_vs_oracle(L, O):
+    """Config 1 at full size through the BVH path (default) against the oracle."""
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, 400, 225)
+    rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, 400, 225, 16, 12, 0.5, 2)
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), 400, 225, 16, 12, 0.5, 2, workers=WORKERS)
+    check(rgb, seg, ref, rseg)
+
+
+def test_bvh_adversarial_spheres(L, O):
+    """Overlapping, nested, duplicated, tiny and huge spheres: ties and grazing hits."""
+    from oracle.oracle import SPHERE_DTYPE
+
+    rng = np.random.default_rng(11)
+    n = 300
+    s = np.zeros(n, dtype=SPHERE_DTYPE)
+    s["center"] = rng.uniform(-3, 3, (n, 3))
+    s["radius"] = np.exp(rng.uniform(np.log(1e-3), np.log(2.0), n))
+    s["material"] = rng.integers(1, 4, n)
+    s["albedo"] = rng.uniform(0.2, 0.95, (n, 3))
+    s["param"] = np.where(s["material"] == 3, 1.5, rng.uniform(0, 0.6, n))
+    s[50:60] = s[40:50]                     # exact duplicates: tie -> lowest index
+    s[60:70] = s[40:50]
+    s["radius"][60:70] *= 0.5               # nested
+    s[0]["center"], s[0]["radius"] = (0, -5000, 0), 4990.0  # huge ground
+    setup = np.array([7.0, 3.0, 6.0, 0, 0, 0, 0, 1, 0, 45.0, 1.0, 9.0, 0.05])
+    st = camera(L, setup, 80, 60)
+    bvh, sb = gpu_render(L, s, DEFAULT_BG, st, 80, 60, 4, 30, 0.5, 9)
+    lin, sl = gpu_render(L, s, DEFAULT_BG, st, 80, 60, 4, 30, 0.5, 9, flags=L.FLAG_LINEAR_SCAN)
+    assert np.array_equal(sb, sl) and np.array_equal(bvh, lin)
+    ref, rseg = O.render(s, DEFAULT_BG, st.as_array(), 80, 60, 4, 30, 0.5, 9, workers=WORKERS)
+    check(bvh, sb, ref, rseg)
+
+
+def test_stats_counters(L, O):
+    import torch
+
+    from tray_amd import ray
+
+    sc = O.rich_scene(2)
+    w, h, spp, depth = 64, 36, 4, 50
+    st = camera(L, RICH_SETUP, w, h)
+    _, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, spp, depth, 0.5, 2, workers=WORKERS)
+    dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
+    out = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+    for flags in (0, L.FLAG_LINEAR_SCAN):
+        stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+        p = L.make_params(w, h, depth, spp, 0.5, 2, flags=flags)
+        dev.render_stats_async(st, p, out.data_ptr(), stats.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        seg, sph, box = stats.tolist()
+        assert seg == int(rseg.sum())
+        if flags:
+            assert sph == seg * len(sc) and box == 0
+        else:
+            assert 0 < sph < seg * len(sc) and box > 0
+    dev.release()

@@ -11,7 +11,9 @@ while [ $# -ge 2 ]; do
   for f in tray_kernel.hip tray_abi.hip; do
     /opt/rocm/bin/hipcc $BASE $FLAGS -c -o $OUT/$f.o csrc/$f & pids+=($!)
   done
-  /opt/rocm/bin/hipcc $BASE $FLAGS -x hip -c -o $OUT/tray_host.cpp.o csrc/tray_host.cpp & pids+=($!)
+  for f in tray_host.cpp tray_bvh.cpp; do
+    /opt/rocm/bin/hipcc $BASE $FLAGS -x hip -c -o $OUT/$f.o csrc/$f & pids+=($!)
+  done
   for p in "${pids[@]}"; do wait $p || { echo "compile failed: $NAME" >&2; exit 1; }; done
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/libtray_amd.so $OUT/*.o
   echo "built $OUT/libtray_amd.so"

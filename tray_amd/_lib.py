@@ -92,7 +92,12 @@ class Params(ctypes.Structure):
         ("tile_count", ctypes.c_int32),
         ("tile_index", ctypes.c_int32),
         ("output", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
+
+
+FLAG_LINEAR_SCAN = 1  # TRAY_FLAG_LINEAR_SCAN
 
 
 class TrayError(RuntimeError):
@@ -117,6 +122,7 @@ EXPORTS = (
     "tray_scene_upload",
     "tray_scene_release",
     "tray_render_async",
+    "tray_render_stats_async",
     "tray_params_rows",
     "tray_to_srgba",
 )
@@ -152,6 +158,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
     L.tray_scene_upload.argtypes = [vp, i32, ctypes.POINTER(Background), i32, ctypes.POINTER(vp)]
     L.tray_scene_release.argtypes = [vp]
     L.tray_render_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
+    L.tray_render_stats_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
     L.tray_params_rows.argtypes = [ctypes.POINTER(Params)]
     L.tray_params_rows.restype = i32
     L.tray_to_srgba.argtypes = [vp, ctypes.c_size_t, vp]
@@ -179,9 +186,9 @@ def spheres_array(spheres) -> np.ndarray:
 
 
 def make_params(width, height, max_depth, rays_per_pixel, ray_radius, seed, y_start=0, y_end=None,
-                tile_rows=0, tile_count=1, tile_index=0, output=OUT_RGB_F64) -> Params:
+                tile_rows=0, tile_count=1, tile_index=0, output=OUT_RGB_F64, flags=0) -> Params:
     return Params(width, height, max_depth, rays_per_pixel, float(ray_radius), int(seed) & (2**64 - 1), y_start,
-                  height if y_end is None else y_end, tile_rows, tile_count, tile_index, output)
+                  height if y_end is None else y_end, tile_rows, tile_count, tile_index, output, flags, 0)
 
 
 def params_rows(p: Params) -> int:
@@ -225,6 +232,14 @@ class DeviceScene:
                      stream: int | None = None) -> None:
         rc = self.L.tray_render_async(self.handle, ctypes.byref(camera), ctypes.byref(params), out_ptr, segments_ptr,
                                       stream)
+        if rc != TRAY_OK:
+            raise TrayError(rc, self.L.tray_last_error().decode())
+
+    def render_stats_async(self, camera: CameraState, params: Params, out_ptr: int, stats_ptr: int,
+                           stream: int | None = None) -> None:
+        """Instrumented render (f32 output); stats_ptr -> 3 x uint64: segments, sphere tests, box tests."""
+        rc = self.L.tray_render_stats_async(self.handle, ctypes.byref(camera), ctypes.byref(params), out_ptr,
+                                            stats_ptr, stream)
         if rc != TRAY_OK:
             raise TrayError(rc, self.L.tray_last_error().decode())
 

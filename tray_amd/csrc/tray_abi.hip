@@ -9,6 +9,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
 #include <mutex>
 #include <string>
@@ -16,6 +17,7 @@
 
 #include "../../include/tray.h"
 #include "tray_internal.hpp"
+#include "bvh.hpp"
 #include "tray_kernel.hpp"
 
 namespace tray {
@@ -97,6 +99,13 @@ struct tray_scene_s {
     tray::MatRec* mat;
     uint32_t* queue;
     tray::V3 bg_a, bg_b;
+    // exact-culling BVH (absent for tiny or non-finite scenes)
+    bool has_bvh;
+    double bvh_bound;
+    int32_t n_nodes, n_slots;
+    tray::BvhNode* nodes;
+    double4* bgeo;
+    int32_t* bidx;
 };
 
 using namespace tray;
@@ -128,6 +137,7 @@ static int validate_params(const tray_params* p) {
         return fail(TRAY_ERR_INVALID_ARGUMENT, "tile_index must be in [0, tile_count)");
     if (p->output < TRAY_OUT_RGB_F64 || p->output > TRAY_OUT_RGBA8)
         return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown output format");
+    if (p->flags & ~TRAY_FLAG_LINEAR_SCAN) return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown flags");
     return TRAY_OK;
 }
 
@@ -196,8 +206,23 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         m.type = s.material;
         m.pad = 0;
     }
+    Bvh bvh;
+    const bool has_bvh = n >= kBvhMinSpheres && build_bvh(spheres, n, &bvh);
+    if (has_bvh) {  // kBvhLeafMax NaN slots so a leaf read of kBvhLeafMax spheres stays in bounds
+        for (int k = 0; k < kBvhLeafMax; ++k) {
+            bvh.geo.push_back(make_double4(qnan, qnan, qnan, qnan));
+            bvh.idx.push_back(0x7fffffff);
+        }
+    }
     tray_scene_s* sc = new tray_scene_s();
     sc->device = device;
+    sc->has_bvh = has_bvh;
+    sc->bvh_bound = bvh.bound;
+    sc->n_nodes = (int32_t)bvh.nodes.size();
+    sc->n_slots = (int32_t)bvh.geo.size();
+    sc->nodes = nullptr;
+    sc->bgeo = nullptr;
+    sc->bidx = nullptr;
     sc->n = n;
     sc->n_pad = n_pad;
     sc->geo = nullptr;
@@ -210,10 +235,24 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     if (e == hipSuccess) e = hipMemcpy(sc->geo, geo.data(), sizeof(double4) * (size_t)n_pad, hipMemcpyHostToDevice);
     if (e == hipSuccess && n > 0) e = hipMalloc(&sc->mat, sizeof(MatRec) * (size_t)n);
     if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && has_bvh) {
+        e = hipMalloc(&sc->nodes, sizeof(BvhNode) * bvh.nodes.size());
+        if (e == hipSuccess) e = hipMalloc(&sc->bgeo, sizeof(double4) * bvh.geo.size());
+        if (e == hipSuccess) e = hipMalloc(&sc->bidx, sizeof(int32_t) * bvh.idx.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->nodes, bvh.nodes.data(), sizeof(BvhNode) * bvh.nodes.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->bgeo, bvh.geo.data(), sizeof(double4) * bvh.geo.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->bidx, bvh.idx.data(), sizeof(int32_t) * bvh.idx.size(), hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
         (void)hipFree(sc->geo);
         (void)hipFree(sc->mat);
         (void)hipFree(sc->queue);
+        (void)hipFree(sc->nodes);
+        (void)hipFree(sc->bgeo);
+        (void)hipFree(sc->bidx);
         delete sc;
         return hip_fail(e, "scene upload");
     }
@@ -227,12 +266,15 @@ int tray_scene_release(tray_scene_t sc) {
     if (sc->geo) (void)hipFree(sc->geo);
     if (sc->mat) (void)hipFree(sc->mat);
     if (sc->queue) (void)hipFree(sc->queue);
+    if (sc->nodes) (void)hipFree(sc->nodes);
+    if (sc->bgeo) (void)hipFree(sc->bgeo);
+    if (sc->bidx) (void)hipFree(sc->bidx);
     delete sc;
     return TRAY_OK;
 }
 
-int tray_render_async(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
-                      uint32_t* segments_device, void* stream) {
+static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
+                             uint32_t* segments_device, unsigned long long* stats_device, void* stream) {
     if (!sc || !cam || !out_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     int rc = validate_params(p);
     if (rc) return rc;
@@ -267,9 +309,37 @@ int tray_render_async(tray_scene_t sc, const tray_camera* cam, const tray_params
     k.bg_b = sc->bg_b;
     k.out = out_device;
     k.segments = segments_device;
+    k.stats = stats_device;
+    k.nodes = sc->nodes;
+    k.bgeo = sc->bgeo;
+    k.bidx = sc->bidx;
+    k.n_nodes = sc->n_nodes;
+    k.n_slots = sc->n_slots;
+    // The BVH's conservative FP32 box test assumes every ray origin lies within
+    // [-M, M]^3 (tray_bvh.cpp): hit points do; check the camera and lens disc.
+    double cam_extent = 0;
+    for (int i = 0; i < 3; ++i) cam_extent = std::max(cam_extent, std::fabs(cam->position[i]));
+    cam_extent += std::fabs(cam->defocus_u[0]) + std::fabs(cam->defocus_u[1]) + std::fabs(cam->defocus_u[2]) +
+                  std::fabs(cam->defocus_v[0]) + std::fabs(cam->defocus_v[1]) + std::fabs(cam->defocus_v[2]);
+    const bool use_bvh = sc->has_bvh && !(p->flags & TRAY_FLAG_LINEAR_SCAN) && cam_extent <= sc->bvh_bound;
     TRAY_HIP(hipSetDevice(sc->device));
-    TRAY_HIP(launch_render(k, static_cast<hipStream_t>(stream)));
+    TRAY_HIP(launch_render(k, use_bvh, static_cast<hipStream_t>(stream)));
     return TRAY_OK;
+}
+
+int tray_render_async(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
+                      uint32_t* segments_device, void* stream) {
+    return render_async_impl(sc, cam, p, out_device, segments_device, nullptr, stream);
+}
+
+int tray_render_stats_async(tray_scene_t sc, const tray_camera* cam, const tray_params* p, float* out_device,
+                            uint64_t* stats_device, void* stream) {
+    if (!stats_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null stats");
+    if (!p) return fail(TRAY_ERR_INVALID_ARGUMENT, "null params");
+    tray_params q = *p;
+    q.output = TRAY_OUT_RGB_F32;
+    return render_async_impl(sc, cam, &q, out_device, nullptr, reinterpret_cast<unsigned long long*>(stats_device),
+                             stream);
 }
 
 int tray_render(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,

@@ -33,6 +33,7 @@
 
 #include <algorithm>
 
+#include "bvh.hpp"
 #include "rng.hpp"
 #include "tray_kernel.hpp"
 
@@ -191,7 +192,8 @@ __device__ __forceinline__ void write_pixel(const KernelParams& p, const Lane& L
 }
 
 // Candidate root of one sphere whose discriminant is >= 0 (Sphere.Hit,
-// ray/objects.go:86-94): the first root inside (1e-6, closest) wins.
+// ray/objects.go:86-94): the first root inside (1e-6, closest) wins. Used by the
+// linear scan, which visits spheres in list order exactly like the reference.
 __device__ __forceinline__ void candidate(double h, double disc, double a, int idx, double& closest, int& best) {
     if (disc >= 0) {
         const double sq = __builtin_sqrt(disc);
@@ -203,6 +205,24 @@ __device__ __forceinline__ void candidate(double h, double disc, double a, int i
         }
         if (ok) {
             closest = root;
+            best = idx;
+        }
+    }
+}
+
+// The same decision for an out-of-order visit. Sphere.Hit's root choice does
+// not depend on the interval end: root2 >= root1, so the reference takes
+// t = root1 if root1 > 1e-6, else root2, and accepts it iff t < closestSoFar.
+// The linear scan therefore returns min over spheres of (t_i, i); accepting
+// "t < closest, or t == closest with a lower index" reproduces it for any order.
+__device__ __forceinline__ void candidate_any_order(double h, double disc, double a, int idx, double& closest,
+                                                    int& best) {
+    if (disc >= 0) {
+        const double sq = __builtin_sqrt(disc);
+        const double r1 = (h - sq) / a;
+        const double t = r1 > 1e-6 ? r1 : (h + sq) / a;
+        if (t > 1e-6 && (t < closest || (t == closest && idx < best))) {
+            closest = t;
             best = idx;
         }
     }
@@ -222,42 +242,37 @@ __device__ __forceinline__ void quad(const double4 g, const D3& org, const D3& d
 #ifndef TRAY_UNROLL
 #define TRAY_UNROLL 8
 #endif
-#ifndef TRAY_PREFETCH
-#define TRAY_PREFETCH 0
-#endif
 
-// Scene.Hit (ray/objects.go:37-46) over geometry padded with NaN spheres (a
-// NaN discriminant is never >= 0). Spheres are tested in groups of U that
-// share one wave-level branch into the (rare) sqrt/div path; inside a group
-// they are visited in list order, so the closest root with the lowest index
-// wins exactly as in the reference's linear scan. With PF the next group is
-// loaded while the current one computes (the padding keeps that in bounds).
-template <int U, bool PF, typename GeoPtr>
-__device__ __forceinline__ int scene_hit(GeoPtr geo, int n, const D3& org, const D3& dir, double& closest) {
+struct Stats {
+    uint32_t spheres = 0, boxes = 0;
+};
+
+// Geometry visible to one workgroup (LDS copies, or global memory when the
+// scene does not fit).
+struct SceneView {
+    const double4* geo;     // linear scan: list order, NaN-padded
+    const BvhNode* nodes;   // BVH: depth-first nodes
+    const double4* bgeo;    // BVH: spheres in leaf-slot order (+4 NaN slots)
+    const int32_t* bidx;    // BVH: original list index of each slot
+    int32_t n, n_nodes;
+};
+
+// Scene.Hit (ray/objects.go:37-46) as the reference's linear scan over
+// NaN-padded geometry (a NaN discriminant is never >= 0). Spheres are tested in
+// groups of U that share one wave-level branch into the rare sqrt/div path;
+// inside a group they are visited in list order.
+template <int U, bool kStats>
+__device__ __forceinline__ int scene_hit_linear(const SceneView& sv, const D3& org, const D3& dir, double& closest,
+                                                Stats& st) {
     const double a = length_sq(dir);  // hoisted: same bits as per sphere
     closest = __builtin_inf();
     int best = -1;
-    const int ngroups = (n + U - 1) / U;
-    double4 nx[U];
-    if constexpr (PF) {
-#pragma unroll
-        for (int k = 0; k < U; ++k) nx[k] = geo[k];
-    }
+    const int ngroups = (sv.n + U - 1) / U;
     for (int gi = 0; gi < ngroups; ++gi) {
         const int i = gi * U;
-        double4 g[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            if constexpr (PF) {
-                g[k] = nx[k];
-                nx[k] = geo[i + U + k];
-            } else {
-                g[k] = geo[i + k];
-            }
-        }
         double h[U], d[U];
 #pragma unroll
-        for (int k = 0; k < U; ++k) quad(g[k], org, dir, a, h[k], d[k]);
+        for (int k = 0; k < U; ++k) quad(sv.geo[i + k], org, dir, a, h[k], d[k]);
         double m = d[0];
 #pragma unroll
         for (int k = 1; k < U; ++k) m = __builtin_fmax(m, d[k]);  // maxNum drops NaN padding
@@ -266,37 +281,95 @@ __device__ __forceinline__ int scene_hit(GeoPtr geo, int n, const D3& org, const
             for (int k = 0; k < U; ++k) candidate(h[k], d[k], a, i + k, closest, best);
         }
     }
+    if constexpr (kStats) st.spheres += (uint32_t)sv.n;
     return best;
 }
 
-// Where the sphere loop reads geometry from: 0 = LDS (staged once per
-// workgroup, broadcast ds_read_b128), 1 = scalar loads through the constant
-// address space (the index is wave-uniform, so the data lands in SGPRs and
-// costs neither LDS bandwidth nor VGPRs).
-#ifndef TRAY_GEO
-#define TRAY_GEO 0
-#endif
-typedef const __attribute__((address_space(4))) double* ConstD;
+// Round a positive (or +inf) double up to a float that is >= it.
+__device__ __forceinline__ float f32_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
 
-// Geometry accessors: element i = {cx, cy, cz, R*R}.
-struct GeoVec {
-    const double4* __restrict__ p;
-    __device__ __forceinline__ double4 operator[](int i) const { return p[i]; }
-};
-struct GeoScalar {
-    ConstD p;
-    __device__ __forceinline__ double4 operator[](int i) const {
-        return make_double4(p[4 * i], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]);
+// Scene.Hit through the exact-culling BVH (tray_bvh.cpp). Per lane, stackless
+// depth-first traversal with skip links. While-while: every lane first advances
+// over nodes (cheap conservative FP32 slab tests on padded boxes, culling
+// against the current closest hit) until it holds a leaf or is done; then the
+// lanes holding a leaf test its <= 4 spheres together in FP64 with the
+// reference's arithmetic and the any-order acceptance rule.
+template <bool kStats>
+__device__ __forceinline__ int scene_hit_bvh(const SceneView& sv, const D3& org, const D3& dir, double& closest,
+                                             Stats& st) {
+    const double a = length_sq(dir);
+    closest = __builtin_inf();
+    int best = -1;
+    float dxf = (float)dir.x, dyf = (float)dir.y, dzf = (float)dir.z;
+    if (__builtin_fabsf(dxf) < 1e-30f) dxf = 1e-30f;
+    if (__builtin_fabsf(dyf) < 1e-30f) dyf = 1e-30f;
+    if (__builtin_fabsf(dzf) < 1e-30f) dzf = 1e-30f;
+    const float ix = 1.0f / dxf, iy = 1.0f / dyf, iz = 1.0f / dzf;
+    const float oix = (float)org.x * ix, oiy = (float)org.y * iy, oiz = (float)org.z * iz;
+    float tlim = __builtin_inff();  // closest rounded up to float
+    int node = 0;
+    while (true) {
+        int leaf = -1;
+        while (true) {
+            const bool search = node < sv.n_nodes && leaf < 0;
+            if (__ballot(search) == 0ull) break;
+            if (search) {
+                const BvhNode nd = sv.nodes[node];
+                const float t0x = __builtin_fmaf(nd.lo[0], ix, -oix), t1x = __builtin_fmaf(nd.hi[0], ix, -oix);
+                const float t0y = __builtin_fmaf(nd.lo[1], iy, -oiy), t1y = __builtin_fmaf(nd.hi[1], iy, -oiy);
+                const float t0z = __builtin_fmaf(nd.lo[2], iz, -oiz), t1z = __builtin_fmaf(nd.hi[2], iz, -oiz);
+                const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                                 __builtin_fmaxf(__builtin_fminf(t0z, t1z), 0.0f));
+                const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                                 __builtin_fminf(__builtin_fmaxf(t0z, t1z), tlim));
+                if constexpr (kStats) ++st.boxes;
+                if (tn <= tf) {
+                    if (nd.leaf >= 0) {
+                        leaf = nd.leaf;
+                        node = nd.skip;
+                    } else {
+                        node = node + 1;
+                    }
+                } else {
+                    node = nd.skip;
+                }
+            }
+        }
+        if (__ballot(leaf >= 0) == 0ull) break;
+        if (leaf >= 0) {
+            const int slot = leaf >> 3, cnt = leaf & 7;
+            double h[kBvhLeafMax], d[kBvhLeafMax];
+#pragma unroll
+            for (int k = 0; k < kBvhLeafMax; ++k) {
+                quad(sv.bgeo[slot + k], org, dir, a, h[k], d[k]);
+                if (k >= cnt) d[k] = __builtin_nan("");
+            }
+            double m = d[0];
+#pragma unroll
+            for (int k = 1; k < kBvhLeafMax; ++k) m = __builtin_fmax(m, d[k]);
+            if (m >= 0) {
+#pragma unroll
+                for (int k = 0; k < kBvhLeafMax; ++k) candidate_any_order(h[k], d[k], a, sv.bidx[slot + k], closest, best);
+                tlim = f32_up(closest);
+            }
+            if constexpr (kStats) st.spheres += (uint32_t)cnt;
+        }
     }
-};
+    return best;
+}
 
 // One Scene.Hit + shading step of the lane's current path (one recursion level
 // of RayColor, ray/objects.go:49-62). Returns true when the path ended.
-template <typename GeoPtr>
-__device__ __forceinline__ bool segment(const KernelParams& p, GeoPtr geo, Lane& L, D3& color) {
+template <bool kBVH, bool kStats>
+__device__ __forceinline__ bool segment(const KernelParams& p, const SceneView& sv, Lane& L, D3& color, Stats& st) {
     ++L.segments;
     double closest;
-    const int best = scene_hit<TRAY_UNROLL, TRAY_PREFETCH != 0>(geo, p.n, L.org, L.dir, closest);
+    const int best = kBVH ? scene_hit_bvh<kStats>(sv, L.org, L.dir, closest, st)
+                          : scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
     if (best < 0) {
         // AmbientLight.Hit (ray/objects.go:68-73)
         const D3 u = unit(L.dir);
@@ -305,7 +378,7 @@ __device__ __forceinline__ bool segment(const KernelParams& p, GeoPtr geo, Lane&
         color = mul(L.thr, sky);
         return true;
     }
-    const double4 g = geo[best];
+    const double4 g = p.geo[best];
     const MatRec m = p.mat[best];
     const D3 point = add(L.org, smul(L.dir, closest));                 // Ray.At (ray/ray.go:23-25)
     const D3 outward = sdiv(sub(point, d3(g.x, g.y, g.z)), m.radius);  // ray/objects.go:100
@@ -370,28 +443,45 @@ __device__ __forceinline__ void start_pixel(const KernelParams& p, Lane& L, int3
     get_ray(p, L.pixel, 0u, L.fx, L.fy, L.org, L.dir);
 }
 
-// Persistent megakernel: waves pull 64-pixel work items from a global counter
-// and lanes refill individually, so no lane idles while the frame has work.
-template <bool kLDS, int kFmt>
 #ifndef TRAY_WAVES_PER_SIMD
 #define TRAY_WAVES_PER_SIMD 5
 #endif
-__global__ __launch_bounds__(256, TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
-    extern __shared__ __attribute__((aligned(16))) double4 s_geo[];
-#if TRAY_GEO == 1
-    const GeoScalar geo{(ConstD)(const double*)p.geo};
-#else
-    GeoVec geo{p.geo};
-    if constexpr (kLDS) {
-        for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) s_geo[i] = p.geo[i];
-        __syncthreads();
-        geo.p = s_geo;
-    }
+#ifndef TRAY_BVH_WAVES_PER_SIMD
+#define TRAY_BVH_WAVES_PER_SIMD 4
 #endif
+
+// Persistent megakernel: waves pull 64-pixel work items from a global counter
+// and lanes refill individually, so no lane idles while the frame has work.
+template <bool kLDS, int kFmt, bool kBVH, bool kStats>
+__global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
+    extern __shared__ __attribute__((aligned(16))) double4 smem[];
+    SceneView sv{p.geo, p.nodes, p.bgeo, p.bidx, p.n, p.n_nodes};
+    if constexpr (kLDS) {
+        if constexpr (kBVH) {
+            // [nodes: n_nodes x 32 B][bgeo: n_slots x 32 B][bidx: n_slots x 4 B]
+            double4* lds_nodes = smem;
+            double4* lds_geo = smem + p.n_nodes;
+            int32_t* lds_idx = reinterpret_cast<int32_t*>(smem + p.n_nodes + p.n_slots);
+            const double4* gn = reinterpret_cast<const double4*>(p.nodes);
+            for (int i = threadIdx.x; i < p.n_nodes; i += blockDim.x) lds_nodes[i] = gn[i];
+            for (int i = threadIdx.x; i < p.n_slots; i += blockDim.x) {
+                lds_geo[i] = p.bgeo[i];
+                lds_idx[i] = p.bidx[i];
+            }
+            sv.nodes = reinterpret_cast<const BvhNode*>(lds_nodes);
+            sv.bgeo = lds_geo;
+            sv.bidx = lds_idx;
+        } else {
+            for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
+            sv.geo = smem;
+        }
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     Lane L;
     L.busy = false;
+    Stats st;
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
     bool exhausted = false;
 
@@ -425,11 +515,17 @@ __global__ __launch_bounds__(256, TRAY_WAVES_PER_SIMD) void render_kernel(Kernel
         if (__ballot(L.busy) == 0ull) break;
         if (L.busy) {
             D3 color;
-            if (segment(p, geo, L, color)) {
+            if (segment<kBVH, kStats>(p, sv, L, color, st)) {
                 L.sum = add(L.sum, color);  // Add(colorSum, color) (ray/tracer.go:143)
                 ++L.sample;
                 if (L.sample >= (uint32_t)p.spp) {
                     write_pixel<kFmt>(p, L);
+                    if constexpr (kStats) {
+                        atomicAdd(p.stats + 0, (unsigned long long)L.segments);
+                        atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
+                        atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
+                        st = Stats{};
+                    }
                     L.busy = false;
                 } else {
                     L.thr = d3(1, 1, 1);
@@ -443,15 +539,20 @@ __global__ __launch_bounds__(256, TRAY_WAVES_PER_SIMD) void render_kernel(Kernel
 
 using KernelFn = void (*)(KernelParams);
 
-static KernelFn pick_kernel(bool use_lds, int fmt) {
-    if (use_lds) {
-        if (fmt == kOutRGBF64) return render_kernel<true, kOutRGBF64>;
-        if (fmt == kOutRGBF32) return render_kernel<true, kOutRGBF32>;
-        return render_kernel<true, kOutRGBA8>;
+template <bool kLDS, bool kBVH, bool kStats>
+static KernelFn pick_fmt(int fmt) {
+    if (fmt == kOutRGBF64) return render_kernel<kLDS, kOutRGBF64, kBVH, kStats>;
+    if (fmt == kOutRGBF32) return render_kernel<kLDS, kOutRGBF32, kBVH, kStats>;
+    return render_kernel<kLDS, kOutRGBA8, kBVH, kStats>;
+}
+
+static KernelFn pick_kernel(bool use_lds, bool bvh, bool stats, int fmt) {
+    if (stats) {  // instrumented launches (bench roofline counts) always write f32
+        if (use_lds) return bvh ? render_kernel<true, kOutRGBF32, true, true> : render_kernel<true, kOutRGBF32, false, true>;
+        return bvh ? render_kernel<false, kOutRGBF32, true, true> : render_kernel<false, kOutRGBF32, false, true>;
     }
-    if (fmt == kOutRGBF64) return render_kernel<false, kOutRGBF64>;
-    if (fmt == kOutRGBF32) return render_kernel<false, kOutRGBF32>;
-    return render_kernel<false, kOutRGBA8>;
+    if (use_lds) return bvh ? pick_fmt<true, true, false>(fmt) : pick_fmt<true, false, false>(fmt);
+    return bvh ? pick_fmt<false, true, false>(fmt) : pick_fmt<false, false, false>(fmt);
 }
 
 // Blocks the device keeps resident for this kernel and LDS size (persistent grid cap).
@@ -467,7 +568,7 @@ static int resident_blocks(int device, KernelFn fn, size_t lds) {
     return cus * per_cu;
 }
 
-hipError_t launch_render(KernelParams p, hipStream_t stream) {
+hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (p.rows <= 0) return hipSuccess;
     p.tiles_x = (p.width + 7) / 8;
     const uint32_t tiles_y = (uint32_t)((p.rows + 7) / 8);
@@ -475,10 +576,12 @@ hipError_t launch_render(KernelParams p, hipStream_t stream) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    const size_t lds_bytes = (size_t)p.n_pad * sizeof(double4);
-    const bool use_lds = TRAY_GEO == 0 && lds_bytes <= kMaxLDSBytes;
-    const size_t lds = use_lds ? lds_bytes : 0;
-    const KernelFn fn = pick_kernel(use_lds, p.out_format);
+    const size_t lds_bytes = use_bvh ? (size_t)p.n_nodes * sizeof(BvhNode) + (size_t)p.n_slots * (sizeof(double4) + 4)
+                                     : (size_t)p.n_pad * sizeof(double4);
+    const bool use_lds = lds_bytes <= kMaxLDSBytes;
+    const size_t lds = use_lds ? (lds_bytes + 15) / 16 * 16 : 0;
+    const bool stats = p.stats != nullptr;
+    const KernelFn fn = pick_kernel(use_lds, use_bvh, stats, p.out_format);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {
         int dev;
@@ -506,6 +609,10 @@ hipError_t launch_render(KernelParams p, hipStream_t stream) {
     const uint32_t grid = std::min<uint32_t>(want, (uint32_t)blocks);
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
+    if (stats) {
+        e = hipMemsetAsync(p.stats, 0, 3 * sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, stream, p);
     return hipGetLastError();
 }

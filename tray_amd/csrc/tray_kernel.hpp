@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "bvh.hpp"
+
 namespace tray {
 
 enum : int32_t { kLambertian = 1, kMetal = 2, kDielectric = 3 };
@@ -47,6 +49,11 @@ struct KernelParams {
     int32_t n_pad;       // round_up(n, 4) + 4
     int32_t tiles_x;     // 8x8 pixel tiles per compact row band
     uint32_t nchunks;    // 64-pixel work items
+    const BvhNode* nodes;   // exact-culling BVH (tray_bvh.cpp), depth-first
+    const double4* bgeo;    // spheres in leaf-slot order, + kBvhLeafMax NaN slots
+    const int32_t* bidx;    // original index per slot
+    int32_t n_nodes, n_slots;
+    unsigned long long* stats;  // nullable: [segments, sphere tests, box tests]
     int32_t width, height, spp, max_depth;
     int32_t y_start, rows, tile_rows, tile_count, tile_index;
     int32_t out_format;
@@ -59,7 +66,7 @@ struct KernelParams {
     uint32_t* segments;
 };
 
-hipError_t launch_render(KernelParams p, hipStream_t stream);
+hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
 
 // Padded geometry length for n spheres (see KernelParams::geo).
 inline int32_t padded_spheres(int32_t n) { return ((n + 3) / 4) * 4 + 4; }
