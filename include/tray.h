@@ -21,22 +21,26 @@
  * ray/materials.go, ray/camera.go). Division and sqrt are correctly rounded.
  *
  * Counter RNG contract (replaces fortio.org/rand v1.1.0, go.mod:9, which is not
- * vendored): every random draw is one Philox4x32-10 block (Salmon et al. 2011,
- * Random123 constants) with
+ * vendored): every random draw comes from one Philox4x32-10 block (Salmon et al.
+ * 2011, Random123 constants) with
  *     key = (seed & 0xffffffff, seed >> 32)
- *     ctr = (pixel, sample, bounce, (purpose << 24) | attempt)
+ *     ctr = (pixel, sample, bounce, purpose << 24)
  *     pixel = y * width + x in GLOBAL image coordinates (tiling-independent)
- *     purpose: 1 = anti-aliasing disc (ray/tracer.go:138), bounce = 0
- *              2 = lens disc (ray/camera.go:128), bounce = 0
- *              3 = scatter draw at hit number `bounce` (ray/materials.go:14,31,57)
- *              4 = host scene generation, ctr = (draw_index, 0, 0, 4 << 24)
- *     u0 = ((x1 << 32 | x0) >> 11) * 2^-53,  u1 = ((x3 << 32 | x2) >> 11) * 2^-53
- * InDisc(r): attempt a = 0..31: x = 2u0-1, y = 2u1-1; accept x*x+y*y < 1 -> (x*r, y*r);
- *            fallback (0,0).
- * UnitVector: attempt a = 0..31 (Marsaglia 1972): x1 = 2u0-1, x2 = 2u1-1,
- *            s = x1*x1+x2*x2; accept 0 < s < 1 -> f = 2*sqrt(1-s), (x1*f, x2*f, 1-2*s);
- *            fallback (0,0,1).
- * Float64 (Dielectric): u0 of attempt 0.
+ *     purpose 1 = the sample's camera block (bounce = 0): words 0,1 feed the
+ *                 anti-aliasing disc (ray/tracer.go:138), words 2,3 the lens
+ *                 disc (ray/camera.go:128)
+ *     purpose 3 = the scatter block of hit number `bounce` (ray/materials.go:14,31,57)
+ *     purpose 4 = host scene generation: ctr = (draw_index, 0, 0, 4 << 24),
+ *                 Float64 = ((x1 << 32 | x0) >> 11) * 2^-53
+ * Renderer uniforms are ui = xi * 2^-32 in [0,1). Samplers (no rejection loops):
+ *     InDisc(r)   = (sqrt(ua) * cos(2 pi ub) * r, sqrt(ua) * sin(2 pi ub) * r)
+ *     UnitVector  = z = 1 - 2 u0, s = sqrt(1 - z*z), (s cos(2 pi u1), s sin(2 pi u1), z)
+ *     Float64     = u0 of the scatter block (Dielectric, ray/materials.go:57)
+ * where sin/cos(2 pi u) is "sincos2pi": quadrant q = floor(4u), f = 4u - q
+ * reflected into [0, 0.5], t = f * (pi/2), Taylor polynomials in t^2 of degree
+ * 15 (sin) and 16 (cos) in Horner form, then the quadrant rotation
+ * (tray_amd/csrc/rng.hpp). Only + - * / sqrt are used, in a fixed order, so the
+ * host oracle and the device produce identical bits.
  * A given (seed, pixel, sample) therefore renders the same colour for any
  * tiling, row range, device count or launch geometry.
  */

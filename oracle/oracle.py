@@ -29,7 +29,7 @@ SPHERE_DTYPE = np.dtype(
 assert SPHERE_DTYPE.itemsize == 72
 
 LAMBERTIAN, METAL, DIELECTRIC = 1, 2, 3
-P_AA, P_LENS, P_SCATTER, P_SCENE = 1, 2, 3, 4
+P_CAMERA, P_SCATTER, P_SCENE = 1, 3, 4
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -65,6 +65,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_unit_vector.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _dp]
         L.oracle_in_disc.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.c_double, _dp]
+        L.oracle_sincos_2pi.argtypes = [ctypes.c_double, _dp]
         L.oracle_reflect.argtypes = [_dp, _dp, _dp]
         L.oracle_refract.argtypes = [_dp, _dp, ctypes.c_double, _dp]
         L.oracle_reflectance.argtypes = [ctypes.c_double, ctypes.c_double]
@@ -126,9 +127,16 @@ def unit_vector(seed, pixel, sample, bounce) -> np.ndarray:
     return o
 
 
-def in_disc(seed, pixel, sample, purpose, radius) -> np.ndarray:
+def in_disc(seed, pixel, sample, which, radius) -> np.ndarray:
+    """which = 0: anti-aliasing disc (camera block words 0,1); 1: lens disc (words 2,3)."""
     o = np.zeros(2)
-    lib().oracle_in_disc(seed, pixel, sample, purpose, radius, _d(o))
+    lib().oracle_in_disc(seed, pixel, sample, which, radius, _d(o))
+    return o
+
+
+def sincos_2pi(u) -> np.ndarray:
+    o = np.zeros(2)
+    lib().oracle_sincos_2pi(u, _d(o))
     return o
 
 

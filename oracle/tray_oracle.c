@@ -146,10 +146,19 @@ static void philox4x32_10(const uint32_t in[4], const uint32_t key[2], uint32_t 
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-enum { P_AA = 1, P_LENS = 2, P_SCATTER = 3, P_SCENE = 4 };
-#define RNG_MAX_ATTEMPTS 32
+enum { P_CAMERA = 1, P_SCATTER = 3, P_SCENE = 4 };
 
-/* Two uniforms in [0,1) with 53-bit resolution from one Philox block. */
+/* One Philox block as four 32-bit uniforms u = x * 2^-32 in [0,1). */
+static void uniforms4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, double u[4]) {
+    uint32_t ctr[4] = {c0, c1, c2, c3};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t x[4];
+    philox4x32_10(ctr, key, x);
+    for (int i = 0; i < 4; ++i) u[i] = (double)x[i] * 0x1.0p-32;
+}
+
+/* Two uniforms in [0,1) with 53-bit resolution from one Philox block (host
+ * scene generation only). */
 static void uniforms2(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, double u[2]) {
     uint32_t ctr[4] = {c0, c1, c2, c3};
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
@@ -161,42 +170,79 @@ static void uniforms2(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint
     u[1] = (double)(b >> 11) * 0x1.0p-53;
 }
 
+/* sin and cos of 2*pi*u for u in [0,1), with + and * only in a fixed order
+ * (include/tray.h "sincos2pi"): quadrant + reflection into [0, pi/4], then
+ * Taylor polynomials (degree 15 / 16) in Horner form. Same bits on any IEEE
+ * double machine without contraction. */
+static void sincos_2pi(double u, double *s, double *c) {
+    double v = u * 4.0;
+    double q = floor(v);
+    double f = v - q;
+    int quad = (int)q;
+    int swap = f > 0.5;
+    double x = swap ? 1.0 - f : f;
+    double t = x * 0x1.921fb54442d18p+0; /* pi/2 */
+    double t2 = t * t;
+    double sp = -0x1.ae7f3e733b81fp-41;         /* -1/15! */
+    sp = sp * t2 + 0x1.6124613a86d09p-33;       /* 1/13! */
+    sp = sp * t2 + -0x1.ae64567f544e4p-26;      /* -1/11! */
+    sp = sp * t2 + 0x1.71de3a556c734p-19;       /* 1/9! */
+    sp = sp * t2 + -0x1.a01a01a01a01ap-13;      /* -1/7! */
+    sp = sp * t2 + 0x1.1111111111111p-7;        /* 1/5! */
+    sp = sp * t2 + -0x1.5555555555555p-3;       /* -1/3! */
+    sp = sp * t2 + 1.0;
+    double sn = t * sp;
+    double cp = 0x1.ae7f3e733b81fp-45;          /* 1/16! */
+    cp = cp * t2 + -0x1.93974a8c07c9dp-37;      /* -1/14! */
+    cp = cp * t2 + 0x1.1eed8eff8d898p-29;       /* 1/12! */
+    cp = cp * t2 + -0x1.27e4fb7789f5cp-22;      /* -1/10! */
+    cp = cp * t2 + 0x1.a01a01a01a01ap-16;       /* 1/8! */
+    cp = cp * t2 + -0x1.6c16c16c16c17p-10;      /* -1/6! */
+    cp = cp * t2 + 0x1.5555555555555p-5;        /* 1/4! */
+    cp = cp * t2 + -0.5;                        /* -1/2! */
+    double cs = cp * t2 + 1.0;
+    if (swap) { double tmp = sn; sn = cs; cs = tmp; }
+    switch (quad & 3) {
+    case 0: *s = sn; *c = cs; break;
+    case 1: *s = cs; *c = -sn; break;
+    case 2: *s = -sn; *c = -cs; break;
+    default: *s = -cs; *c = sn; break;
+    }
+}
+
 typedef struct { uint64_t seed; uint32_t pixel; uint32_t sample; } rngkey;
 
-/* InDisc(radius) replacement (ray/tracer.go:138, ray/camera.go:128): rejection
- * sampling of the unit disc, scaled by radius. */
-static void in_disc(rngkey k, uint32_t purpose, double radius, double *ox, double *oy) {
-    for (uint32_t a = 0; a < RNG_MAX_ATTEMPTS; ++a) {
-        double u[2];
-        uniforms2(k.seed, k.pixel, k.sample, 0u, (purpose << 24) | a, u);
-        double x = 2.0 * u[0] - 1.0;
-        double y = 2.0 * u[1] - 1.0;
-        if (x * x + y * y < 1.0) { *ox = x * radius; *oy = y * radius; return; }
-    }
-    *ox = 0.0; *oy = 0.0;
+/* InDisc(radius) replacement (ray/tracer.go:138, ray/camera.go:128): polar map
+ * of two uniforms of the sample's camera block; which = 0 (anti-aliasing,
+ * words 0,1) or 1 (lens, words 2,3). */
+static void in_disc(rngkey k, int which, double radius, double *ox, double *oy) {
+    double u[4];
+    uniforms4(k.seed, k.pixel, k.sample, 0u, (uint32_t)P_CAMERA << 24, u);
+    double r = sqrt(u[2 * which]);
+    double s, c;
+    sincos_2pi(u[2 * which + 1], &s, &c);
+    *ox = (r * c) * radius;
+    *oy = (r * s) * radius;
 }
 
-/* RandomUnitVector (ray/rand.go:30-32 -> rand.UnitVector): Marsaglia (1972)
- * uniform direction on S^2 using only + - * / sqrt. */
+/* RandomUnitVector (ray/rand.go:30-32 -> rand.UnitVector): uniform on S^2 by
+ * Archimedes' projection, z = 1 - 2u0, phi = 2 pi u1, from the bounce's
+ * scatter block. */
 static vec3 random_unit_vector(rngkey k, uint32_t bounce) {
-    for (uint32_t a = 0; a < RNG_MAX_ATTEMPTS; ++a) {
-        double u[2];
-        uniforms2(k.seed, k.pixel, k.sample, bounce, ((uint32_t)P_SCATTER << 24) | a, u);
-        double x1 = 2.0 * u[0] - 1.0;
-        double x2 = 2.0 * u[1] - 1.0;
-        double s = x1 * x1 + x2 * x2;
-        if (s < 1.0 && s > 0.0) {
-            double f = 2.0 * sqrt(1.0 - s);
-            return V(x1 * f, x2 * f, 1.0 - 2.0 * s);
-        }
-    }
-    return V(0.0, 0.0, 1.0);
+    double u[4];
+    uniforms4(k.seed, k.pixel, k.sample, bounce, (uint32_t)P_SCATTER << 24, u);
+    double z = 1.0 - 2.0 * u[0];
+    double r = sqrt(1.0 - z * z);
+    double s, c;
+    sincos_2pi(u[1], &s, &c);
+    return V(r * c, r * s, z);
 }
 
-/* rIn.Float64() in Dielectric.Scatter (ray/materials.go:57). */
+/* rIn.Float64() in Dielectric.Scatter (ray/materials.go:57): word 0 of the
+ * bounce's scatter block. */
 static double random_float64(rngkey k, uint32_t bounce) {
-    double u[2];
-    uniforms2(k.seed, k.pixel, k.sample, bounce, ((uint32_t)P_SCATTER << 24), u);
+    double u[4];
+    uniforms4(k.seed, k.pixel, k.sample, bounce, (uint32_t)P_SCATTER << 24, u);
     return u[0];
 }
 
@@ -362,7 +408,7 @@ static ray get_ray(const o_camera *c, rngkey k, double px, double py, double ox,
     r.dir = sub(sample, pos);
     if (c->aperture > 0) {
         double dx, dy;
-        in_disc(k, P_LENS, 1.0, &dx, &dy);
+        in_disc(k, 1, 1.0, &dx, &dy);
         vec3 du = V(c->defocus_u[0], c->defocus_u[1], c->defocus_u[2]);
         vec3 dv = V(c->defocus_v[0], c->defocus_v[1], c->defocus_v[2]);
         vec3 offset = add(smul(du, dx), smul(dv, dy));
@@ -391,7 +437,7 @@ static int render_pixel(const scene *sc, const o_camera *cam, const o_params *p,
     for (int s = 0; s < p->spp; ++s) {
         rngkey k = {p->seed, (uint32_t)y * (uint32_t)p->width + (uint32_t)x, (uint32_t)s};
         double ox = 0.0, oy = 0.0;
-        if (multiple_rays) in_disc(k, P_AA, p->ray_radius, &ox, &oy);
+        if (multiple_rays) in_disc(k, 0, p->ray_radius, &ox, &oy);
         ray r = get_ray(cam, k, (double)x, (double)y, ox, oy);
         vec3 c = ray_color(sc, &r, p->max_depth, k, 0u, &segs, &err);
         if (err) return -2;
@@ -528,11 +574,12 @@ ORACLE_EXPORT void oracle_unit_vector(uint64_t seed, uint32_t pixel, uint32_t sa
     vec3 v = random_unit_vector(k, bounce);
     out[0] = v.x; out[1] = v.y; out[2] = v.z;
 }
-ORACLE_EXPORT void oracle_in_disc(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t purpose,
-                                  double radius, double out[2]) {
+ORACLE_EXPORT void oracle_in_disc(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t which, double radius,
+                                  double out[2]) {
     rngkey k = {seed, pixel, sample};
-    in_disc(k, purpose, radius, &out[0], &out[1]);
+    in_disc(k, (int)which, radius, &out[0], &out[1]);
 }
+ORACLE_EXPORT void oracle_sincos_2pi(double u, double out[2]) { sincos_2pi(u, &out[0], &out[1]); }
 ORACLE_EXPORT void oracle_reflect(const double v[3], const double n[3], double out[3]) {
     vec3 r = reflect(V(v[0], v[1], v[2]), V(n[0], n[1], n[2]));
     out[0] = r.x; out[1] = r.y; out[2] = r.z;

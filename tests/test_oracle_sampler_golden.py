@@ -22,13 +22,35 @@ def test_unit_vector_distribution(O):  # ray/vec3_test.go:539-649 (100k samples)
     assert np.all(np.abs(z_hist - n / 20) <= 0.1 * n / 20)
 
 
-@pytest.mark.parametrize("purpose,radius", [(1, 0.5), (2, 1.0), (1, 1.0)])
-def test_in_disc(O, purpose, radius):  # InDisc: inside the disc, uniform over its area
-    d = np.array([O.in_disc(3, i, 0, purpose, radius) for i in range(40_000)])
+@pytest.mark.parametrize("which,radius", [(0, 0.5), (1, 1.0), (0, 1.0)])
+def test_in_disc(O, which, radius):  # InDisc: inside the disc, uniform over its area
+    d = np.array([O.in_disc(3, i, 0, which, radius) for i in range(40_000)])
     r2 = (d**2).sum(1)
     assert np.all(r2 < radius * radius)
     assert abs(r2.mean() / (radius * radius) - 0.5) < 0.01  # E[r^2] = R^2/2 for a uniform disc
     assert np.all(np.abs(d.mean(0)) < 0.01 * radius)
+
+
+def test_sincos_2pi(O):
+    """The contract's sin/cos(2 pi u): + and * only, accurate to a few ulps."""
+    us = np.concatenate([np.linspace(0, 1, 4001, endpoint=False), np.random.default_rng(1).random(4000),
+                         [0.125, 0.25 - 2**-40, 0.5, 0.75, 1 - 2**-32]])
+    got = np.array([O.sincos_2pi(u) for u in us])
+    assert np.max(np.abs(got[:, 0] - np.sin(2 * np.pi * us))) < 1e-15  # np side rounds 2*pi*u too
+    assert np.max(np.abs(got[:, 1] - np.cos(2 * np.pi * us))) < 1e-15
+    assert tuple(O.sincos_2pi(0.0)) == (0.0, 1.0) and tuple(O.sincos_2pi(0.25)) == (1.0, -0.0)
+
+
+def test_camera_block_shared(O):
+    """AA (words 0,1) and lens (words 2,3) discs come from one Philox block per sample."""
+    a = O.in_disc(5, 77, 3, 0, 1.0)
+    b = O.in_disc(5, 77, 3, 1, 1.0)
+    assert tuple(a) != tuple(b)
+    ctr = (77, 3, 0, 1 << 24)
+    x = O.philox4x32_10(ctr, (5, 0))
+    u = [v * 2.0**-32 for v in x]
+    s, c = O.sincos_2pi(u[1])
+    assert tuple(a) == ((u[0] ** 0.5 * c) * 1.0, (u[0] ** 0.5 * s) * 1.0)
 
 
 @pytest.mark.parametrize("name", ["rngfree_mirrors", "rngfree_mirrors_deep"])

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase cycle split of the BVH kernel from a -DTRAY_PROFILE
+build (tools/build_variants.sh prof "-DTRAY_PROFILE"). Not a timing tool: the
+stamps serialise phases; read the SHARES.
+
+    python tools/phase_profile.py path/to/libtray_amd.so [--config c2]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("lib")
+    ap.add_argument("--config", default="c2")
+    args = ap.parse_args()
+    import torch
+
+    from bench import CONFIGS
+    from tray_amd import _lib, ray
+
+    label, seed, half, W, H, spp, depth = CONFIGS[args.config]
+    spheres = ray.rich_scene_array(seed, half)
+    cam = ray.RichSceneCamera()
+    cam.Initialize(W, H)
+    scene = _lib.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0, os.path.abspath(args.lib))
+    params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    stats = torch.zeros(16, dtype=torch.int64, device="cuda")
+    scene.render_stats_async(cam._state, params, out.data_ptr(), stats.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    v = stats.tolist()
+    names = ["segments", "sphere_tests", "box_tests", "cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade",
+             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters"]
+    d = dict(zip(names, v))
+    cyc = sum(d[k] for k in ("cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade"))
+    d["share"] = {k: round(d[k] / cyc, 3) for k in ("cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade")}
+    d["lanes_per_node_iter"] = round(d["node_lanes"] / max(1, d["node_iters"]), 1)
+    d["lanes_per_leaf_phase"] = round(d["leaf_lanes"] / max(1, d["leaf_phases"]), 1)
+    d["lanes_per_shade_phase"] = round(d["shade_lanes"] / max(1, d["shade_phases"]), 1)
+    d["cyc_per_node_iter"] = round(d["cyc_node"] / max(1, d["node_iters"]), 1)
+    d["cyc_per_leaf_phase"] = round(d["cyc_leaf"] / max(1, d["leaf_phases"]), 1)
+    d["cyc_per_shade_phase"] = round(d["cyc_shade"] / max(1, d["shade_phases"]), 1)
+    print(json.dumps(d))
+
+
+if __name__ == "__main__":
+    main()

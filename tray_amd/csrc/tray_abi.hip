@@ -106,6 +106,7 @@ struct tray_scene_s {
     tray::BvhNode* nodes;
     double4* bgeo;
     int32_t* bidx;
+    tray::MatRec* bmat;
 };
 
 using namespace tray;
@@ -223,6 +224,13 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->nodes = nullptr;
     sc->bgeo = nullptr;
     sc->bidx = nullptr;
+    sc->bmat = nullptr;
+    std::vector<MatRec> bmat(bvh.idx.size());
+    for (size_t i = 0; i < bvh.idx.size(); ++i) {
+        const int32_t k = bvh.idx[i];
+        if (k >= 0 && k < n) bmat[i] = mat[(size_t)k];
+        else memset(&bmat[i], 0, sizeof(MatRec));
+    }
     sc->n = n;
     sc->n_pad = n_pad;
     sc->geo = nullptr;
@@ -245,6 +253,9 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
             e = hipMemcpy(sc->bgeo, bvh.geo.data(), sizeof(double4) * bvh.geo.size(), hipMemcpyHostToDevice);
         if (e == hipSuccess)
             e = hipMemcpy(sc->bidx, bvh.idx.data(), sizeof(int32_t) * bvh.idx.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc(&sc->bmat, sizeof(MatRec) * bmat.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->bmat, bmat.data(), sizeof(MatRec) * bmat.size(), hipMemcpyHostToDevice);
     }
     if (e != hipSuccess) {
         (void)hipFree(sc->geo);
@@ -253,6 +264,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         (void)hipFree(sc->nodes);
         (void)hipFree(sc->bgeo);
         (void)hipFree(sc->bidx);
+        (void)hipFree(sc->bmat);
         delete sc;
         return hip_fail(e, "scene upload");
     }
@@ -269,6 +281,7 @@ int tray_scene_release(tray_scene_t sc) {
     if (sc->nodes) (void)hipFree(sc->nodes);
     if (sc->bgeo) (void)hipFree(sc->bgeo);
     if (sc->bidx) (void)hipFree(sc->bidx);
+    if (sc->bmat) (void)hipFree(sc->bmat);
     delete sc;
     return TRAY_OK;
 }
@@ -313,6 +326,7 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.nodes = sc->nodes;
     k.bgeo = sc->bgeo;
     k.bidx = sc->bidx;
+    k.bmat = sc->bmat;
     k.n_nodes = sc->n_nodes;
     k.n_slots = sc->n_slots;
     // The BVH's conservative FP32 box test assumes every ray origin lies within

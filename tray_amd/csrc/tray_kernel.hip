@@ -86,43 +86,36 @@ __device__ __forceinline__ double reflectance(double cosine, double ref_idx) {
     return r0 + (1 - r0) * (x * x4);
 }
 
-__device__ __forceinline__ void in_disc(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t purpose,
-                                        double radius, double& ox, double& oy) {
-    ox = 0.0;
-    oy = 0.0;
-    for (uint32_t a = 0; a < kMaxAttempts; ++a) {
-        const U2 u = philox_uniforms(seed, pixel, sample, 0u, (purpose << 24) | a);
-        const double x = 2.0 * u.u0 - 1.0;
-        const double y = 2.0 * u.u1 - 1.0;
-        if (x * x + y * y < 1.0) {
-            ox = x * radius;
-            oy = y * radius;
-            break;
-        }
-    }
+// InDisc(radius) (ray/tracer.go:138, ray/camera.go:128): polar map of two
+// uniforms: r = sqrt(ua), phi = 2 pi ub.
+__device__ __forceinline__ void disc(double ua, double ub, double radius, double& ox, double& oy) {
+    const double r = __builtin_sqrt(ua);
+    double s, c;
+    sincos_2pi(ub, s, c);
+    ox = (r * c) * radius;
+    oy = (r * s) * radius;
 }
 
+// RandomUnitVector (ray/rand.go:30-32): Archimedes' projection of the bounce's
+// scatter block, z = 1 - 2 u0, phi = 2 pi u1.
 __device__ __forceinline__ D3 unit_vector(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce) {
-    D3 r = d3(0.0, 0.0, 1.0);
-    for (uint32_t a = 0; a < kMaxAttempts; ++a) {
-        const U2 u = philox_uniforms(seed, pixel, sample, bounce, (kPurposeScatter << 24) | a);
-        const double x1 = 2.0 * u.u0 - 1.0;
-        const double x2 = 2.0 * u.u1 - 1.0;
-        const double s = x1 * x1 + x2 * x2;
-        if (s < 1.0 && s > 0.0) {
-            const double f = 2.0 * __builtin_sqrt(1.0 - s);
-            r = d3(x1 * f, x2 * f, 1.0 - 2.0 * s);
-            break;
-        }
-    }
-    return r;
+    const U4 u = philox_u4(seed, pixel, sample, bounce, kPurposeScatter << 24);
+    const double z = 1.0 - 2.0 * u.u0;
+    const double r = __builtin_sqrt(1.0 - z * z);
+    double s, c;
+    sincos_2pi(u.u1, s, c);
+    return d3(r * c, r * s, z);
 }
 
-// Camera.GetRay (ray/camera.go:113-142).
+// Camera.GetRay (ray/camera.go:113-142). The sample's camera block feeds the
+// anti-aliasing disc (words 0,1; ray/tracer.go:136-139) and the lens disc
+// (words 2,3).
 __device__ __forceinline__ void get_ray(const KernelParams& p, uint32_t pixel, uint32_t sample, double px, double py,
                                         D3& origin, D3& dir) {
     double ox = 0.0, oy = 0.0;
-    if (p.spp > 1) in_disc(p.seed, pixel, sample, kPurposeAA, p.ray_radius, ox, oy);  // ray/tracer.go:136-139
+    U4 u = U4{0, 0, 0, 0};
+    if (p.spp > 1 || p.cam.aperture > 0) u = philox_u4(p.seed, pixel, sample, 0u, kPurposeCamera << 24);
+    if (p.spp > 1) disc(u.u0, u.u1, p.ray_radius, ox, oy);
     const D3 pos = d3(p.cam.position[0], p.cam.position[1], p.cam.position[2]);
     const D3 p00 = d3(p.cam.pixel00[0], p.cam.pixel00[1], p.cam.pixel00[2]);
     const D3 pxv = d3(p.cam.pixel_x[0], p.cam.pixel_x[1], p.cam.pixel_x[2]);
@@ -132,7 +125,7 @@ __device__ __forceinline__ void get_ray(const KernelParams& p, uint32_t pixel, u
     dir = sub(sample_pt, pos);
     if (p.cam.aperture > 0) {
         double dx, dy;
-        in_disc(p.seed, pixel, sample, kPurposeLens, 1.0, dx, dy);
+        disc(u.u2, u.u3, 1.0, dx, dy);
         const D3 du = d3(p.cam.defocus_u[0], p.cam.defocus_u[1], p.cam.defocus_u[2]);
         const D3 dv = d3(p.cam.defocus_v[0], p.cam.defocus_v[1], p.cam.defocus_v[2]);
         const D3 offset = add(smul(du, dx), smul(dv, dy));
@@ -254,6 +247,7 @@ struct SceneView {
     const BvhNode* nodes;   // BVH: depth-first nodes
     const double4* bgeo;    // BVH: spheres in leaf-slot order (+4 NaN slots)
     const int32_t* bidx;    // BVH: original list index of each slot
+    const MatRec* bmat;     // BVH: shading record of each slot
     int32_t n, n_nodes;
 };
 
@@ -292,84 +286,102 @@ __device__ __forceinline__ float f32_up(double v) {
     return f;
 }
 
-// Scene.Hit through the exact-culling BVH (tray_bvh.cpp). Per lane, stackless
-// depth-first traversal with skip links. While-while: every lane first advances
-// over nodes (cheap conservative FP32 slab tests on padded boxes, culling
-// against the current closest hit) until it holds a leaf or is done; then the
-// lanes holding a leaf test its <= 4 spheres together in FP64 with the
-// reference's arithmetic and the any-order acceptance rule.
-template <bool kStats>
-__device__ __forceinline__ int scene_hit_bvh(const SceneView& sv, const D3& org, const D3& dir, double& closest,
-                                             Stats& st) {
-    const double a = length_sq(dir);
-    closest = __builtin_inf();
-    int best = -1;
+// Per-lane traversal state of one Scene.Hit through the exact-culling BVH
+// (tray_bvh.cpp): stackless depth-first walk with skip links, conservative FP32
+// slab tests on padded boxes (culled against the current closest hit), FP64
+// sphere tests with the reference's arithmetic and the any-order acceptance rule.
+// Lane states of the BVH kernel.
+enum : uint32_t { kIdleState = 0, kTravState = 1, kLeafState = 2, kShadeState = 3 };
+
+struct Trav {
+    float ix, iy, iz, oix, oiy, oiz;  // FP32 ray: t = box * inv - org * inv
+    float tlim;                       // closest rounded up to float
+    int32_t node, leaf;
+    double a, closest;
+    int32_t best;  // original list index of the closest hit (tie-break key)
+    int32_t slot;  // its leaf slot (LDS-resident geometry + shading record)
+};
+
+__device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir) {
+    T.a = length_sq(dir);  // hoisted: same bits as per sphere
+    T.closest = __builtin_inf();
+    T.best = -1;
+    T.slot = 0;
+    T.tlim = __builtin_inff();
+    T.node = 0;
+    T.leaf = -1;
     float dxf = (float)dir.x, dyf = (float)dir.y, dzf = (float)dir.z;
     if (__builtin_fabsf(dxf) < 1e-30f) dxf = 1e-30f;
     if (__builtin_fabsf(dyf) < 1e-30f) dyf = 1e-30f;
     if (__builtin_fabsf(dzf) < 1e-30f) dzf = 1e-30f;
-    const float ix = 1.0f / dxf, iy = 1.0f / dyf, iz = 1.0f / dzf;
-    const float oix = (float)org.x * ix, oiy = (float)org.y * iy, oiz = (float)org.z * iz;
-    float tlim = __builtin_inff();  // closest rounded up to float
-    int node = 0;
-    while (true) {
-        int leaf = -1;
-        while (true) {
-            const bool search = node < sv.n_nodes && leaf < 0;
-            if (__ballot(search) == 0ull) break;
-            if (search) {
-                const BvhNode nd = sv.nodes[node];
-                const float t0x = __builtin_fmaf(nd.lo[0], ix, -oix), t1x = __builtin_fmaf(nd.hi[0], ix, -oix);
-                const float t0y = __builtin_fmaf(nd.lo[1], iy, -oiy), t1y = __builtin_fmaf(nd.hi[1], iy, -oiy);
-                const float t0z = __builtin_fmaf(nd.lo[2], iz, -oiz), t1z = __builtin_fmaf(nd.hi[2], iz, -oiz);
-                const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
-                                                 __builtin_fmaxf(__builtin_fminf(t0z, t1z), 0.0f));
-                const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
-                                                 __builtin_fminf(__builtin_fmaxf(t0z, t1z), tlim));
-                if constexpr (kStats) ++st.boxes;
-                if (tn <= tf) {
-                    if (nd.leaf >= 0) {
-                        leaf = nd.leaf;
-                        node = nd.skip;
-                    } else {
-                        node = node + 1;
-                    }
-                } else {
-                    node = nd.skip;
-                }
-            }
-        }
-        if (__ballot(leaf >= 0) == 0ull) break;
-        if (leaf >= 0) {
-            const int slot = leaf >> 3, cnt = leaf & 7;
-            double h[kBvhLeafMax], d[kBvhLeafMax];
-#pragma unroll
-            for (int k = 0; k < kBvhLeafMax; ++k) {
-                quad(sv.bgeo[slot + k], org, dir, a, h[k], d[k]);
-                if (k >= cnt) d[k] = __builtin_nan("");
-            }
-            double m = d[0];
-#pragma unroll
-            for (int k = 1; k < kBvhLeafMax; ++k) m = __builtin_fmax(m, d[k]);
-            if (m >= 0) {
-#pragma unroll
-                for (int k = 0; k < kBvhLeafMax; ++k) candidate_any_order(h[k], d[k], a, sv.bidx[slot + k], closest, best);
-                tlim = f32_up(closest);
-            }
-            if constexpr (kStats) st.spheres += (uint32_t)cnt;
-        }
-    }
-    return best;
+    // ~1 ulp reciprocal: inside the padding's error budget (tray_bvh.cpp)
+    T.ix = __builtin_amdgcn_rcpf(dxf);
+    T.iy = __builtin_amdgcn_rcpf(dyf);
+    T.iz = __builtin_amdgcn_rcpf(dzf);
+    T.oix = (float)org.x * T.ix;
+    T.oiy = (float)org.y * T.iy;
+    T.oiz = (float)org.z * T.iz;
 }
 
-// One Scene.Hit + shading step of the lane's current path (one recursion level
-// of RayColor, ray/objects.go:49-62). Returns true when the path ended.
-template <bool kBVH, bool kStats>
-__device__ __forceinline__ bool segment(const KernelParams& p, const SceneView& sv, Lane& L, D3& color, Stats& st) {
-    ++L.segments;
-    double closest;
-    const int best = kBVH ? scene_hit_bvh<kStats>(sv, L.org, L.dir, closest, st)
-                          : scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
+// One node visit. Returns the new lane state: kTrav, kLeaf (holds T.leaf) or
+// kShade (traversal finished).
+__device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv) {
+    const uint4* np = reinterpret_cast<const uint4*>(sv.nodes + T.node);
+    const uint4 q0 = np[0], q1 = np[1];
+    const float lox = __uint_as_float(q0.x), loy = __uint_as_float(q0.y), loz = __uint_as_float(q0.z);
+    const float hix = __uint_as_float(q0.w), hiy = __uint_as_float(q1.x), hiz = __uint_as_float(q1.y);
+    const int32_t skip = (int32_t)q1.z, leaf = (int32_t)q1.w;
+    const float t0x = __builtin_fmaf(lox, T.ix, -T.oix), t1x = __builtin_fmaf(hix, T.ix, -T.oix);
+    const float t0y = __builtin_fmaf(loy, T.iy, -T.oiy), t1y = __builtin_fmaf(hiy, T.iy, -T.oiy);
+    const float t0z = __builtin_fmaf(loz, T.iz, -T.oiz), t1z = __builtin_fmaf(hiz, T.iz, -T.oiz);
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                     __builtin_fmaxf(__builtin_fminf(t0z, t1z), 0.0f));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                     __builtin_fminf(__builtin_fmaxf(t0z, t1z), T.tlim));
+    const bool hit = tn <= tf;
+    T.node = (hit && leaf < 0) ? T.node + 1 : skip;
+    if (hit && leaf >= 0) {
+        T.leaf = leaf;
+        return kLeafState;
+    }
+    return T.node < sv.n_nodes ? kTravState : kShadeState;
+}
+
+// Test the held leaf's <= kBvhLeafMax spheres (FP64, any-order rule).
+__device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const D3& org, const D3& dir) {
+    const int slot = T.leaf >> 3, cnt = T.leaf & 7;
+    double h[kBvhLeafMax], d[kBvhLeafMax];
+#pragma unroll
+    for (int k = 0; k < kBvhLeafMax; ++k) {
+        quad(sv.bgeo[slot + k], org, dir, T.a, h[k], d[k]);
+        if (k >= cnt) d[k] = __builtin_nan("");
+    }
+    double m = d[0];
+#pragma unroll
+    for (int k = 1; k < kBvhLeafMax; ++k) m = __builtin_fmax(m, d[k]);
+    if (m >= 0) {
+#pragma unroll
+        for (int k = 0; k < kBvhLeafMax; ++k) {
+            const int32_t idx = sv.bidx[slot + k];
+            const int32_t before = T.best;
+            candidate_any_order(h[k], d[k], T.a, idx, T.closest, T.best);
+            if (T.best != before) T.slot = slot + k;
+        }
+        T.tlim = f32_up(T.closest);
+    }
+    T.leaf = -1;
+    return T.node < sv.n_nodes ? kTravState : kShadeState;
+}
+
+// Shading of one Scene.Hit result (one recursion level of RayColor,
+// ray/objects.go:49-62): sky on a miss, else the hit record and the material's
+// scatter. `g`/`mrec` give the hit sphere's geometry and shading record (LDS
+// for the BVH kernel, global memory for the linear scan). Returns true when the
+// path ended (its colour in `color`); otherwise the lane's ray, throughput and
+// bounce advance to the scattered ray.
+template <typename GeoAt, typename MatAt>
+__device__ __forceinline__ bool shade(const KernelParams& p, Lane& L, int best, double closest, GeoAt geo_at,
+                                      MatAt mat_at, D3& color) {
     if (best < 0) {
         // AmbientLight.Hit (ray/objects.go:68-73)
         const D3 u = unit(L.dir);
@@ -378,8 +390,8 @@ __device__ __forceinline__ bool segment(const KernelParams& p, const SceneView& 
         color = mul(L.thr, sky);
         return true;
     }
-    const double4 g = p.geo[best];
-    const MatRec m = p.mat[best];
+    const double4 g = geo_at();
+    const MatRec m = mat_at();
     const D3 point = add(L.org, smul(L.dir, closest));                 // Ray.At (ray/ray.go:23-25)
     const D3 outward = sdiv(sub(point, d3(g.x, g.y, g.z)), m.radius);  // ray/objects.go:100
     const bool front = dot(L.dir, outward) < 0;                        // SetFaceNormal (:19-26)
@@ -404,7 +416,7 @@ __device__ __forceinline__ bool segment(const KernelParams& p, const SceneView& 
         const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
         bool do_reflect = ratio * sin_theta > 1.0;  // cannot refract
         if (!do_reflect) {
-            const U2 u = philox_uniforms(p.seed, L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
+            const U4 u = philox_u4(p.seed, L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
             do_reflect = reflectance(cos_theta, ratio) > u.u0;
         }
         new_dir = do_reflect ? reflect(ud, normal) : refract(ud, normal, ratio);
@@ -443,33 +455,95 @@ __device__ __forceinline__ void start_pixel(const KernelParams& p, Lane& L, int3
     get_ray(p, L.pixel, 0u, L.fx, L.fy, L.org, L.dir);
 }
 
+// A path ended with `color`: accumulate (Add(colorSum, color), ray/tracer.go:143)
+// and either start the next sample or finish the pixel. Returns false when the
+// pixel is done (written) and the lane is free.
+template <int kFmt, bool kStats>
+__device__ __forceinline__ bool end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st) {
+    L.sum = add(L.sum, color);
+    ++L.sample;
+    if (L.sample >= (uint32_t)p.spp) {
+        write_pixel<kFmt>(p, L);
+        if constexpr (kStats) {
+            atomicAdd(p.stats + 0, (unsigned long long)L.segments);
+            atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
+            atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
+            st = Stats{};
+        }
+        L.busy = false;
+        return false;
+    }
+    L.thr = d3(1, 1, 1);
+    L.bounce = 0;
+    get_ray(p, L.pixel, L.sample, L.fx, L.fy, L.org, L.dir);
+    return true;
+}
+
 #ifndef TRAY_WAVES_PER_SIMD
 #define TRAY_WAVES_PER_SIMD 5
 #endif
 #ifndef TRAY_BVH_WAVES_PER_SIMD
-#define TRAY_BVH_WAVES_PER_SIMD 4
+#define TRAY_BVH_WAVES_PER_SIMD 3
+#endif
+// BVH lane scheduling: node steps per loop iteration, and how many lanes must
+// be waiting before the (expensive, FP64) leaf and shading phases run. A phase
+// also runs whenever nothing else can make progress.
+#ifndef TRAY_NODE_STEPS
+#define TRAY_NODE_STEPS 2
+#endif
+#ifndef TRAY_LEAF_BATCH
+#define TRAY_LEAF_BATCH 24
+#endif
+#ifndef TRAY_SHADE_BATCH
+#define TRAY_SHADE_BATCH 32
+#endif
+
+// Diagnostic build only (-DTRAY_PROFILE): per-wave s_memtime stamps around each
+// phase of the BVH loop, plus phase and active-lane counts, added into
+// stats[3..15] (the stats buffer must then hold 16 counters). Never part of a
+// timed build: the stamps' waits serialise the phases.
+#ifdef TRAY_PROFILE
+#define PROF_T0() const uint64_t prof_t0_ = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(slot) prof[slot] += __builtin_amdgcn_s_memtime() - prof_t0_
+#define PROF_CNT(slot, v) prof[slot] += (v)
+#else
+#define PROF_T0()
+#define PROF_ADD(slot)
+#define PROF_CNT(slot, v)
 #endif
 
 // Persistent megakernel: waves pull 64-pixel work items from a global counter
 // and lanes refill individually, so no lane idles while the frame has work.
+//
+// Linear scan (kBVH = false): each loop iteration is one Scene.Hit + shading
+// step for every busy lane.
+// BVH (kBVH = true): each lane is a small state machine (traverse a node / test
+// a leaf / shade) and one loop iteration runs a few cheap node steps for the
+// traversing lanes, then the leaf phase and the shading phase only once enough
+// lanes wait for them. A lane whose traversal ends early does not wait for the
+// wave's slowest ray: it shades and starts its next segment while others still
+// traverse.
 template <bool kLDS, int kFmt, bool kBVH, bool kStats>
 __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
     extern __shared__ __attribute__((aligned(16))) double4 smem[];
-    SceneView sv{p.geo, p.nodes, p.bgeo, p.bidx, p.n, p.n_nodes};
+    SceneView sv{p.geo, p.nodes, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
     if constexpr (kLDS) {
         if constexpr (kBVH) {
-            // [nodes: n_nodes x 32 B][bgeo: n_slots x 32 B][bidx: n_slots x 4 B]
+            // [nodes: n_nodes x 32 B][bgeo: n_slots x 32 B][bmat: n_slots x 48 B][bidx: n_slots x 4 B]
             double4* lds_nodes = smem;
             double4* lds_geo = smem + p.n_nodes;
-            int32_t* lds_idx = reinterpret_cast<int32_t*>(smem + p.n_nodes + p.n_slots);
+            MatRec* lds_mat = reinterpret_cast<MatRec*>(smem + p.n_nodes + p.n_slots);
+            int32_t* lds_idx = reinterpret_cast<int32_t*>(lds_mat + p.n_slots);
             const double4* gn = reinterpret_cast<const double4*>(p.nodes);
             for (int i = threadIdx.x; i < p.n_nodes; i += blockDim.x) lds_nodes[i] = gn[i];
             for (int i = threadIdx.x; i < p.n_slots; i += blockDim.x) {
                 lds_geo[i] = p.bgeo[i];
+                lds_mat[i] = p.bmat[i];
                 lds_idx[i] = p.bidx[i];
             }
             sv.nodes = reinterpret_cast<const BvhNode*>(lds_nodes);
             sv.bgeo = lds_geo;
+            sv.bmat = lds_mat;
             sv.bidx = lds_idx;
         } else {
             for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
@@ -482,11 +556,18 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
     Lane L;
     L.busy = false;
     Stats st;
+    Trav T;
+    uint32_t state = kIdleState;
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
     bool exhausted = false;
+#ifdef TRAY_PROFILE
+    uint64_t prof[13] = {};
+#endif
 
     while (true) {
+        PROF_CNT(10, 1);
         // Refill idle lanes from the wave's pool, fetching 64-item chunks from the global queue.
+        PROF_T0();
         uint64_t idle = __ballot(!L.busy);
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
@@ -506,35 +587,90 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                 const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
                 if (rank < take) {
                     int32_t x, j;
-                    if (decode_pixel(p, pool_next + rank, x, j)) start_pixel(p, L, x, j);
+                    if (decode_pixel(p, pool_next + rank, x, j)) {
+                        start_pixel(p, L, x, j);
+                        if constexpr (kBVH) {
+                            ++L.segments;
+                            trav_begin(T, L.org, L.dir);
+                            state = sv.n_nodes > 0 ? kTravState : kShadeState;
+                        }
+                    }
                 }
             }
             pool_next += take;
             idle = __ballot(!L.busy);
         }
+        PROF_ADD(0);
         if (__ballot(L.busy) == 0ull) break;
-        if (L.busy) {
-            D3 color;
-            if (segment<kBVH, kStats>(p, sv, L, color, st)) {
-                L.sum = add(L.sum, color);  // Add(colorSum, color) (ray/tracer.go:143)
-                ++L.sample;
-                if (L.sample >= (uint32_t)p.spp) {
-                    write_pixel<kFmt>(p, L);
-                    if constexpr (kStats) {
-                        atomicAdd(p.stats + 0, (unsigned long long)L.segments);
-                        atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
-                        atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
-                        st = Stats{};
+
+        if constexpr (!kBVH) {
+            if (L.busy) {
+                ++L.segments;
+                double closest;
+                const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
+                D3 color;
+                if (shade(p, L, best, closest, [&] { return p.geo[best]; }, [&] { return p.mat[best]; }, color))
+                    end_path<kFmt, kStats>(p, L, color, st);
+            }
+        } else {
+            // Node steps for the traversing lanes.
+            {
+                PROF_T0();
+#pragma unroll 1
+                for (int s = 0; s < TRAY_NODE_STEPS; ++s) {
+                    const uint64_t m = __ballot(state == kTravState);
+                    if (m == 0ull) break;
+                    PROF_CNT(4, 1);
+                    PROF_CNT(5, __popcll(m));
+                    if (state == kTravState) {
+                        state = trav_node(T, sv);
+                        if constexpr (kStats) ++st.boxes;
                     }
-                    L.busy = false;
-                } else {
-                    L.thr = d3(1, 1, 1);
-                    L.bounce = 0;
-                    get_ray(p, L.pixel, L.sample, L.fx, L.fy, L.org, L.dir);
                 }
+                PROF_ADD(1);
+            }
+            // Leaf phase: FP64 sphere tests, batched.
+            const uint64_t m_leaf = __ballot(state == kLeafState);
+            if (m_leaf != 0ull &&
+                (__popcll(m_leaf) >= TRAY_LEAF_BATCH || __ballot(state == kTravState) == 0ull)) {
+                PROF_T0();
+                PROF_CNT(6, 1);
+                PROF_CNT(7, __popcll(m_leaf));
+                if (state == kLeafState) {
+                    if constexpr (kStats) st.spheres += (uint32_t)(T.leaf & 7);
+                    state = trav_leaf(T, sv, L.org, L.dir);
+                }
+                PROF_ADD(2);
+            }
+            // Shading phase, batched.
+            const uint64_t m_shade = __ballot(state == kShadeState);
+            if (m_shade != 0ull && (__popcll(m_shade) >= TRAY_SHADE_BATCH ||
+                                    __ballot(state == kTravState || state == kLeafState) == 0ull)) {
+                PROF_T0();
+                PROF_CNT(8, 1);
+                PROF_CNT(9, __popcll(m_shade));
+                if (state == kShadeState) {
+                    D3 color;
+                    bool more = true;
+                    if (shade(p, L, T.best, T.closest, [&] { return sv.bgeo[T.slot]; },
+                              [&] { return sv.bmat[T.slot]; }, color))
+                        more = end_path<kFmt, kStats>(p, L, color, st);
+                    if (more) {
+                        ++L.segments;
+                        trav_begin(T, L.org, L.dir);
+                        state = kTravState;
+                    } else {
+                        state = kIdleState;
+                    }
+                }
+                PROF_ADD(3);
             }
         }
     }
+#ifdef TRAY_PROFILE
+    if (kStats && lane == 0)
+        for (int i = 0; i < 13; ++i) atomicAdd(p.stats + 3 + i, (unsigned long long)prof[i]);
+#endif
 }
 
 using KernelFn = void (*)(KernelParams);
@@ -576,7 +712,8 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    const size_t lds_bytes = use_bvh ? (size_t)p.n_nodes * sizeof(BvhNode) + (size_t)p.n_slots * (sizeof(double4) + 4)
+    const size_t lds_bytes = use_bvh ? (size_t)p.n_nodes * sizeof(BvhNode) +
+                                           (size_t)p.n_slots * (sizeof(double4) + sizeof(MatRec) + 4)
                                      : (size_t)p.n_pad * sizeof(double4);
     const bool use_lds = lds_bytes <= kMaxLDSBytes;
     const size_t lds = use_lds ? (lds_bytes + 15) / 16 * 16 : 0;
@@ -610,7 +747,11 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (stats) {
+#ifdef TRAY_PROFILE
+        e = hipMemsetAsync(p.stats, 0, 16 * sizeof(unsigned long long), stream);
+#else
         e = hipMemsetAsync(p.stats, 0, 3 * sizeof(unsigned long long), stream);
+#endif
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, stream, p);

@@ -52,6 +52,7 @@ struct KernelParams {
     const BvhNode* nodes;   // exact-culling BVH (tray_bvh.cpp), depth-first
     const double4* bgeo;    // spheres in leaf-slot order, + kBvhLeafMax NaN slots
     const int32_t* bidx;    // original index per slot
+    const MatRec* bmat;     // shading record per slot
     int32_t n_nodes, n_slots;
     unsigned long long* stats;  // nullable: [segments, sphere tests, box tests]
     int32_t width, height, spp, max_depth;
