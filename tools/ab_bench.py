@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--linear", action="store_true", help="force the linear-scan kernel")
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
     import numpy as np
@@ -31,7 +32,8 @@ def main():
     cam = ray.RichSceneCamera()
     cam.Initialize(W, H)
     bg = ray._background(ray.DefaultBackground())
-    params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
+    params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32,
+                              flags=_lib.FLAG_LINEAR_SCAN if args.linear else 0)
     stream = torch.cuda.current_stream()
     runs = {}
     for v in args.variants:

@@ -10,6 +10,7 @@ import json
 import os
 import sys
 
+PHASES = ("cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade", "cyc_gen")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -31,22 +32,24 @@ def main():
     scene = _lib.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0, os.path.abspath(args.lib))
     params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
     out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-    stats = torch.zeros(16, dtype=torch.int64, device="cuda")
+    stats = torch.zeros(19, dtype=torch.int64, device="cuda")
     scene.render_stats_async(cam._state, params, out.data_ptr(), stats.data_ptr(),
                              torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     v = stats.tolist()
     names = ["segments", "sphere_tests", "box_tests", "cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade",
-             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters"]
+             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "gen_phases", "gen_lanes", "cyc_gen"]
     d = dict(zip(names, v))
-    cyc = sum(d[k] for k in ("cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade"))
-    d["share"] = {k: round(d[k] / cyc, 3) for k in ("cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade")}
+    cyc = sum(d[k] for k in PHASES)
+    d["share"] = {k: round(d[k] / cyc, 3) for k in PHASES}
     d["lanes_per_node_iter"] = round(d["node_lanes"] / max(1, d["node_iters"]), 1)
     d["lanes_per_leaf_phase"] = round(d["leaf_lanes"] / max(1, d["leaf_phases"]), 1)
     d["lanes_per_shade_phase"] = round(d["shade_lanes"] / max(1, d["shade_phases"]), 1)
     d["cyc_per_node_iter"] = round(d["cyc_node"] / max(1, d["node_iters"]), 1)
     d["cyc_per_leaf_phase"] = round(d["cyc_leaf"] / max(1, d["leaf_phases"]), 1)
     d["cyc_per_shade_phase"] = round(d["cyc_shade"] / max(1, d["shade_phases"]), 1)
+    d["lanes_per_gen_phase"] = round(d["gen_lanes"] / max(1, d["gen_phases"]), 1)
+    d["cyc_per_gen_phase"] = round(d["cyc_gen"] / max(1, d["gen_phases"]), 1)
     print(json.dumps(d))
 
 

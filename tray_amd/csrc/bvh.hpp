@@ -33,6 +33,6 @@ struct Bvh {
 };
 
 // Returns false on non-finite input (the caller then uses the linear scan).
-bool build_bvh(const tray_sphere* spheres, int32_t n, Bvh* out);
+bool build_bvh(const tray_sphere* spheres, int32_t n, Bvh* out, int leaf_max = kBvhLeafMax);
 
 }  // namespace tray

@@ -204,6 +204,8 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         m.albedo[2] = s.albedo[2];
         m.param = s.param;
         m.radius = s.radius;
+        m.rinv = 1.0 / s.radius;  // correctly rounded on the host
+        m.pinv = 1.0 / s.param;
         m.type = s.material;
         m.pad = 0;
     }

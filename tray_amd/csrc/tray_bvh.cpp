@@ -59,6 +59,7 @@ struct Builder {
     std::vector<double4> geo;
     std::vector<int32_t> idx;
     double pad = 0;
+    int leaf_max = kBvhLeafMax;
 
     static float down(double v) {
         float f = (float)v;
@@ -82,7 +83,7 @@ struct Builder {
             nodes[me].hi[k] = up(box.hi[k] + pad);
         }
         const int count = e - b;
-        if (count <= kBvhLeafMax) {
+        if (count <= leaf_max) {
             const int slot = (int)geo.size();
             for (int i = b; i < e; ++i) {
                 const tray_sphere& sp = s[prims[i].index];
@@ -176,7 +177,7 @@ struct Builder {
 
 }  // namespace
 
-bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out) {
+bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     out->nodes.clear();
     out->geo.clear();
     out->idx.clear();
@@ -199,6 +200,7 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out) {
     }
     m = std::max(m, 1.0);
     B.pad = 4e-6 * m;
+    B.leaf_max = std::min(std::max(leaf_max, 1), kBvhLeafMax);
     out->bound = m;
     B.build(0, n, s);
     out->nodes.swap(B.nodes);

@@ -51,11 +51,32 @@ __device__ __forceinline__ D3 smul(D3 v, double t) { return d3(v.x * t, v.y * t,
 __device__ __forceinline__ D3 mul(D3 u, D3 v) { return d3(u.x * v.x, u.y * v.y, u.z * v.z); }
 __device__ __forceinline__ D3 sdiv(D3 v, double t) { return d3(v.x / t, v.y / t, v.z / t); }
 __device__ __forceinline__ D3 neg(D3 v) { return d3(-v.x, -v.y, -v.z); }
+
+// a / b, correctly rounded, given y = RN(1/b) (exactly rounded, e.g. a full
+// division or a host-side 1.0/b): q = RN(a*y) is within 1 ulp of a/b, the
+// residual fma(-b, q, a) is exact, and one correction fma(r, y, q) returns
+// RN(a/b) (Markstein 1990; Muller et al., Handbook of Floating-Point Arithmetic
+// §4.7). 3 FP64 instructions instead of ~10 for the generic sequence; checked
+// on 10^9 pairs by tools/div_check.hip. Zero keeps its sign, and quotients near
+// the overflow/underflow range (or non-finite operands) take the full division.
+__device__ __forceinline__ double div_rcp(double a, double b, double y) {
+    const double q = a * y;
+    const double r = __builtin_fma(-b, q, a);
+    const double q1 = __builtin_fma(r, y, q);
+    const double aq = __builtin_fabs(q);
+    if (a == 0) return q;
+    if (!(aq > 0x1p-960 && aq < 0x1p+960)) return a / b;
+    return q1;
+}
+__device__ __forceinline__ D3 sdiv_rcp(D3 v, double t, double y) {
+    return d3(div_rcp(v.x, t, y), div_rcp(v.y, t, y), div_rcp(v.z, t, y));
+}
 __device__ __forceinline__ double dot(D3 u, D3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
 __device__ __forceinline__ double length_sq(D3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
+// Unit (ray/vec3.go:116-119): each component divided by the length.
 __device__ __forceinline__ D3 unit(D3 v) {
     const double l = __builtin_sqrt(length_sq(v));
-    return d3(v.x / l, v.y / l, v.z / l);
+    return sdiv_rcp(v, l, 1.0 / l);
 }
 __device__ __forceinline__ bool near_zero(D3 v) {
     const double s = 1e-8;
@@ -96,10 +117,36 @@ __device__ __forceinline__ void disc(double ua, double ub, double radius, double
     oy = (r * s) * radius;
 }
 
-// RandomUnitVector (ray/rand.go:30-32): Archimedes' projection of the bounce's
-// scatter block, z = 1 - 2 u0, phi = 2 pi u1.
-__device__ __forceinline__ D3 unit_vector(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce) {
-    const U4 u = philox_u4(seed, pixel, sample, bounce, kPurposeScatter << 24);
+// Camera and background, copied once per workgroup into LDS and read through a
+// volatile pointer where needed: keeps ~50 dwords of loop-invariant kernel
+// arguments out of the SGPR file (they otherwise spill to VGPR lanes and cost a
+// v_readlane on every use).
+struct Uniforms {
+    CamRec cam;
+    V3 bg_a, bg_b;
+    double focus_time, ray_radius;
+    uint64_t seed;
+};
+// Explicit LDS address space: a generic volatile pointer would be accessed with
+// (slow, system-coherent) flat loads.
+typedef const volatile __attribute__((address_space(3))) Uniforms* UniPtr;
+
+// The RNG key, re-read per draw and made wave-uniform: Philox's round keys are
+// then recomputed with scalar adds instead of being hoisted out of the loop
+// (where they would be spilled to VGPR lanes and cost a v_readlane each).
+__device__ __forceinline__ uint64_t uni_seed(UniPtr uni) {
+    const uint64_t s = uni->seed;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)s);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(s >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+constexpr size_t kUniformsBytes = (sizeof(Uniforms) + 255) / 256 * 256;
+
+__device__ __forceinline__ D3 ld3(const volatile __attribute__((address_space(3))) double* v) { return d3(v[0], v[1], v[2]); }
+
+// RandomUnitVector (ray/rand.go:30-32): Archimedes' projection of two uniforms of
+// the bounce's scatter block, z = 1 - 2 u0, phi = 2 pi u1.
+__device__ __forceinline__ D3 unit_vector_from(const U4& u) {
     const double z = 1.0 - 2.0 * u.u0;
     const double r = __builtin_sqrt(1.0 - z * z);
     double s, c;
@@ -107,29 +154,33 @@ __device__ __forceinline__ D3 unit_vector(uint64_t seed, uint32_t pixel, uint32_
     return d3(r * c, r * s, z);
 }
 
-// Camera.GetRay (ray/camera.go:113-142). The sample's camera block feeds the
-// anti-aliasing disc (words 0,1; ray/tracer.go:136-139) and the lens disc
-// (words 2,3).
-__device__ __forceinline__ void get_ray(const KernelParams& p, uint32_t pixel, uint32_t sample, double px, double py,
+// The sample's camera block (purpose 1): (pixel, sample, 0, 1<<24).
+__device__ __forceinline__ U4 camera_block(UniPtr uni, uint32_t pixel, uint32_t sample) {
+    return philox_u4(uni_seed(uni), pixel, sample, 0u, kPurposeCamera << 24);
+}
+
+// Camera.GetRay (ray/camera.go:113-142). The sample's camera block `u` feeds the
+// anti-aliasing disc (words 0,1; ray/tracer.go:136-139, only when r > 1) and the
+// lens disc (words 2,3, only when the aperture is open).
+__device__ __forceinline__ void get_ray(const KernelParams& p, UniPtr uni, const U4& u, double px, double py,
                                         D3& origin, D3& dir) {
     double ox = 0.0, oy = 0.0;
-    U4 u = U4{0, 0, 0, 0};
-    if (p.spp > 1 || p.cam.aperture > 0) u = philox_u4(p.seed, pixel, sample, 0u, kPurposeCamera << 24);
-    if (p.spp > 1) disc(u.u0, u.u1, p.ray_radius, ox, oy);
-    const D3 pos = d3(p.cam.position[0], p.cam.position[1], p.cam.position[2]);
-    const D3 p00 = d3(p.cam.pixel00[0], p.cam.pixel00[1], p.cam.pixel00[2]);
-    const D3 pxv = d3(p.cam.pixel_x[0], p.cam.pixel_x[1], p.cam.pixel_x[2]);
-    const D3 pyv = d3(p.cam.pixel_y[0], p.cam.pixel_y[1], p.cam.pixel_y[2]);
+    const double aperture = uni->cam.aperture;
+    if (p.spp > 1) disc(u.u0, u.u1, uni->ray_radius, ox, oy);
+    const D3 pos = ld3(uni->cam.position);
+    const D3 p00 = ld3(uni->cam.pixel00);
+    const D3 pxv = ld3(uni->cam.pixel_x);
+    const D3 pyv = ld3(uni->cam.pixel_y);
     const D3 sample_pt = add(add(p00, smul(pxv, px + ox)), smul(pyv, py + oy));
     origin = pos;
     dir = sub(sample_pt, pos);
-    if (p.cam.aperture > 0) {
+    if (aperture > 0) {
         double dx, dy;
         disc(u.u2, u.u3, 1.0, dx, dy);
-        const D3 du = d3(p.cam.defocus_u[0], p.cam.defocus_u[1], p.cam.defocus_u[2]);
-        const D3 dv = d3(p.cam.defocus_v[0], p.cam.defocus_v[1], p.cam.defocus_v[2]);
+        const D3 du = ld3(uni->cam.defocus_u);
+        const D3 dv = ld3(uni->cam.defocus_v);
         const D3 offset = add(smul(du, dx), smul(dv, dy));
-        const D3 focus_point = add(pos, smul(dir, p.focus_time));
+        const D3 focus_point = add(pos, smul(dir, uni->focus_time));
         origin = add(pos, offset);
         dir = sub(focus_point, origin);
     }
@@ -187,13 +238,14 @@ __device__ __forceinline__ void write_pixel(const KernelParams& p, const Lane& L
 // Candidate root of one sphere whose discriminant is >= 0 (Sphere.Hit,
 // ray/objects.go:86-94): the first root inside (1e-6, closest) wins. Used by the
 // linear scan, which visits spheres in list order exactly like the reference.
-__device__ __forceinline__ void candidate(double h, double disc, double a, int idx, double& closest, int& best) {
+__device__ __forceinline__ void candidate(double h, double disc, double a, double a_inv, int idx, double& closest,
+                                          int& best) {
     if (disc >= 0) {
         const double sq = __builtin_sqrt(disc);
-        double root = (h - sq) / a;
+        double root = div_rcp(h - sq, a, a_inv);
         bool ok = root > 1e-6 && root < closest;
         if (!ok) {
-            root = (h + sq) / a;
+            root = div_rcp(h + sq, a, a_inv);
             ok = root > 1e-6 && root < closest;
         }
         if (ok) {
@@ -208,12 +260,12 @@ __device__ __forceinline__ void candidate(double h, double disc, double a, int i
 // t = root1 if root1 > 1e-6, else root2, and accepts it iff t < closestSoFar.
 // The linear scan therefore returns min over spheres of (t_i, i); accepting
 // "t < closest, or t == closest with a lower index" reproduces it for any order.
-__device__ __forceinline__ void candidate_any_order(double h, double disc, double a, int idx, double& closest,
-                                                    int& best) {
+__device__ __forceinline__ void candidate_any_order(double h, double disc, double a, double a_inv, int idx,
+                                                    double& closest, int& best) {
     if (disc >= 0) {
         const double sq = __builtin_sqrt(disc);
-        const double r1 = (h - sq) / a;
-        const double t = r1 > 1e-6 ? r1 : (h + sq) / a;
+        const double r1 = div_rcp(h - sq, a, a_inv);
+        const double t = r1 > 1e-6 ? r1 : div_rcp(h + sq, a, a_inv);
         if (t > 1e-6 && (t < closest || (t == closest && idx < best))) {
             closest = t;
             best = idx;
@@ -236,8 +288,9 @@ __device__ __forceinline__ void quad(const double4 g, const D3& org, const D3& d
 #define TRAY_UNROLL 8
 #endif
 
+// Instrumented launches only: per-lane counters, flushed once when the lane exits.
 struct Stats {
-    uint32_t spheres = 0, boxes = 0;
+    uint64_t segments = 0, spheres = 0, boxes = 0;
 };
 
 // Geometry visible to one workgroup (LDS copies, or global memory when the
@@ -259,6 +312,7 @@ template <int U, bool kStats>
 __device__ __forceinline__ int scene_hit_linear(const SceneView& sv, const D3& org, const D3& dir, double& closest,
                                                 Stats& st) {
     const double a = length_sq(dir);  // hoisted: same bits as per sphere
+    const double a_inv = 1.0 / a;
     closest = __builtin_inf();
     int best = -1;
     const int ngroups = (sv.n + U - 1) / U;
@@ -272,10 +326,10 @@ __device__ __forceinline__ int scene_hit_linear(const SceneView& sv, const D3& o
         for (int k = 1; k < U; ++k) m = __builtin_fmax(m, d[k]);  // maxNum drops NaN padding
         if (m >= 0) {
 #pragma unroll
-            for (int k = 0; k < U; ++k) candidate(h[k], d[k], a, i + k, closest, best);
+            for (int k = 0; k < U; ++k) candidate(h[k], d[k], a, a_inv, i + k, closest, best);
         }
     }
-    if constexpr (kStats) st.spheres += (uint32_t)sv.n;
+    if constexpr (kStats) st.spheres += (uint64_t)sv.n;
     return best;
 }
 
@@ -297,13 +351,14 @@ struct Trav {
     float ix, iy, iz, oix, oiy, oiz;  // FP32 ray: t = box * inv - org * inv
     float tlim;                       // closest rounded up to float
     int32_t node, leaf;
-    double a, closest;
+    double a, a_inv, closest;
     int32_t best;  // original list index of the closest hit (tie-break key)
     int32_t slot;  // its leaf slot (LDS-resident geometry + shading record)
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir) {
     T.a = length_sq(dir);  // hoisted: same bits as per sphere
+    T.a_inv = 1.0 / T.a;
     T.closest = __builtin_inf();
     T.best = -1;
     T.slot = 0;
@@ -347,6 +402,9 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv) {
     return T.node < sv.n_nodes ? kTravState : kShadeState;
 }
 
+#ifndef TRAY_LEAF_COMPACT
+#define TRAY_LEAF_COMPACT 1
+#endif
 // Test the held leaf's <= kBvhLeafMax spheres (FP64, any-order rule).
 __device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const D3& org, const D3& dir) {
     const int slot = T.leaf >> 3, cnt = T.leaf & 7;
@@ -356,6 +414,31 @@ __device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, cons
         quad(sv.bgeo[slot + k], org, dir, T.a, h[k], d[k]);
         if (k >= cnt) d[k] = __builtin_nan("");
     }
+#if TRAY_LEAF_COMPACT
+    // Only spheres whose discriminant is >= 0 need the root (a sqrt and two
+    // divisions): each lane walks its own candidates, so the wave pays for
+    // max-over-lanes(candidates) roots instead of kBvhLeafMax.
+    uint32_t cand = 0;
+#pragma unroll
+    for (int k = 0; k < kBvhLeafMax; ++k) cand |= (d[k] >= 0) ? (1u << k) : 0u;
+    if (cand != 0u) {
+        while (cand != 0u) {
+            const int k = __builtin_ctz(cand);
+            cand &= cand - 1u;
+            double hk = h[0], dk = d[0];
+#pragma unroll
+            for (int q = 1; q < kBvhLeafMax; ++q) {
+                hk = k == q ? h[q] : hk;
+                dk = k == q ? d[q] : dk;
+            }
+            const int32_t idx = sv.bidx[slot + k];
+            const int32_t before = T.best;
+            candidate_any_order(hk, dk, T.a, T.a_inv, idx, T.closest, T.best);
+            if (T.best != before) T.slot = slot + k;
+        }
+        T.tlim = f32_up(T.closest);
+    }
+#else
     double m = d[0];
 #pragma unroll
     for (int k = 1; k < kBvhLeafMax; ++k) m = __builtin_fmax(m, d[k]);
@@ -364,70 +447,14 @@ __device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, cons
         for (int k = 0; k < kBvhLeafMax; ++k) {
             const int32_t idx = sv.bidx[slot + k];
             const int32_t before = T.best;
-            candidate_any_order(h[k], d[k], T.a, idx, T.closest, T.best);
+            candidate_any_order(h[k], d[k], T.a, T.a_inv, idx, T.closest, T.best);
             if (T.best != before) T.slot = slot + k;
         }
         T.tlim = f32_up(T.closest);
     }
+#endif
     T.leaf = -1;
     return T.node < sv.n_nodes ? kTravState : kShadeState;
-}
-
-// Shading of one Scene.Hit result (one recursion level of RayColor,
-// ray/objects.go:49-62): sky on a miss, else the hit record and the material's
-// scatter. `g`/`mrec` give the hit sphere's geometry and shading record (LDS
-// for the BVH kernel, global memory for the linear scan). Returns true when the
-// path ended (its colour in `color`); otherwise the lane's ray, throughput and
-// bounce advance to the scattered ray.
-template <typename GeoAt, typename MatAt>
-__device__ __forceinline__ bool shade(const KernelParams& p, Lane& L, int best, double closest, GeoAt geo_at,
-                                      MatAt mat_at, D3& color) {
-    if (best < 0) {
-        // AmbientLight.Hit (ray/objects.go:68-73)
-        const D3 u = unit(L.dir);
-        const double t = 0.5 * (u.y + 1.0);
-        const D3 sky = add(smul(d3(p.bg_a.x, p.bg_a.y, p.bg_a.z), 1.0 - t), smul(d3(p.bg_b.x, p.bg_b.y, p.bg_b.z), t));
-        color = mul(L.thr, sky);
-        return true;
-    }
-    const double4 g = geo_at();
-    const MatRec m = mat_at();
-    const D3 point = add(L.org, smul(L.dir, closest));                 // Ray.At (ray/ray.go:23-25)
-    const D3 outward = sdiv(sub(point, d3(g.x, g.y, g.z)), m.radius);  // ray/objects.go:100
-    const bool front = dot(L.dir, outward) < 0;                        // SetFaceNormal (:19-26)
-    const D3 normal = front ? outward : neg(outward);
-    bool scattered = true;
-    D3 new_dir;
-    D3 att = d3(m.albedo[0], m.albedo[1], m.albedo[2]);
-    if (m.type == kLambertian) {  // ray/materials.go:13-20
-        new_dir = add(normal, unit_vector(p.seed, L.pixel, L.sample, L.bounce));
-        if (near_zero(new_dir)) new_dir = normal;
-    } else if (m.type == kMetal) {  // ray/materials.go:28-37
-        D3 reflected = reflect(unit(L.dir), normal);
-        if (m.param > 0.0)
-            reflected = add(reflected, smul(unit_vector(p.seed, L.pixel, L.sample, L.bounce), m.param));
-        new_dir = reflected;
-        scattered = dot(new_dir, normal) > 0;
-    } else {  // Dielectric, ray/materials.go:44-64
-        att = d3(1.0, 1.0, 1.0);
-        const double ratio = front ? 1.0 / m.param : m.param;
-        const D3 ud = unit(L.dir);
-        const double cos_theta = go_min(dot(neg(ud), normal), 1.0);
-        const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
-        bool do_reflect = ratio * sin_theta > 1.0;  // cannot refract
-        if (!do_reflect) {
-            const U4 u = philox_u4(p.seed, L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
-            do_reflect = reflectance(cos_theta, ratio) > u.u0;
-        }
-        new_dir = do_reflect ? reflect(ud, normal) : refract(ud, normal, ratio);
-    }
-    color = d3(0, 0, 0);
-    if (!scattered) return true;  // absorbed -> black
-    L.thr = mul(L.thr, att);
-    L.org = point;
-    L.dir = new_dir;
-    ++L.bounce;
-    return L.bounce >= (uint32_t)p.max_depth;  // RayColor(depth 0) -> black
 }
 
 // Work item w (64 pixels = one 8x8 tile of the compact row space) -> pixel.
@@ -439,6 +466,8 @@ __device__ __forceinline__ bool decode_pixel(const KernelParams& p, uint32_t ite
     return x < p.width && j < p.rows;
 }
 
+// Claim pixel (x, compact row j) for the lane; its first camera ray is generated
+// by the caller (get_ray, directly or in the BVH kernel's batched phase).
 __device__ __forceinline__ void start_pixel(const KernelParams& p, Lane& L, int32_t x, int32_t j) {
     const int32_t y = row_of(p, j);
     L.x = x;
@@ -452,30 +481,95 @@ __device__ __forceinline__ void start_pixel(const KernelParams& p, Lane& L, int3
     L.thr = d3(1, 1, 1);
     L.sum = d3(0, 0, 0);
     L.busy = true;
-    get_ray(p, L.pixel, 0u, L.fx, L.fy, L.org, L.dir);
 }
 
 // A path ended with `color`: accumulate (Add(colorSum, color), ray/tracer.go:143)
-// and either start the next sample or finish the pixel. Returns false when the
+// and either set up the next sample or finish the pixel. Returns false when the
 // pixel is done (written) and the lane is free.
 template <int kFmt, bool kStats>
-__device__ __forceinline__ bool end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st) {
+__device__ __forceinline__ bool finish_sample(const KernelParams& p, Lane& L, const D3& color, Stats& st) {
     L.sum = add(L.sum, color);
     ++L.sample;
     if (L.sample >= (uint32_t)p.spp) {
         write_pixel<kFmt>(p, L);
-        if constexpr (kStats) {
-            atomicAdd(p.stats + 0, (unsigned long long)L.segments);
-            atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
-            atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
-            st = Stats{};
-        }
+        if constexpr (kStats) st.segments += L.segments;
         L.busy = false;
         return false;
     }
     L.thr = d3(1, 1, 1);
     L.bounce = 0;
-    get_ray(p, L.pixel, L.sample, L.fx, L.fy, L.org, L.dir);
+    return true;
+}
+
+// One recursion level of RayColor (ray/objects.go:49-62) after Scene.Hit gave
+// (best, closest): the sky on a miss, else the hit record and the material's
+// scatter; a path that ends is accumulated and the lane moves on to its next
+// sample's camera ray. `geo_at`/`mat_at` give the hit sphere's geometry and
+// shading record. Returns true when the lane has a new ray to trace, false when
+// its pixel is finished (written) and the lane is free.
+//
+// Written for a wave of lanes on different branches: the work every branch
+// needs is done once, before the branches — one Philox block per lane (the
+// bounce's scatter block, or the next sample's camera block when the path ends
+// here) and the unit direction (sky, Metal, Dielectric).
+template <int kFmt, bool kStats, typename GeoAt, typename MatAt>
+__device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
+                                           GeoAt geo_at, MatAt mat_at, Stats& st) {
+    const bool hit = best >= 0;
+    // A hit at the last level ends the path black whatever its material does
+    // (RayColor(depth 0) is black), so no scatter is computed for it.
+    const bool last = L.bounce + 1u >= (uint32_t)p.max_depth;
+    bool ends = !hit || last;
+    U4 u = philox_u4(uni_seed(uni), L.pixel, ends ? L.sample + 1u : L.sample, ends ? 0u : L.bounce,
+                     (ends ? kPurposeCamera : kPurposeScatter) << 24);
+    const D3 ud = unit(L.dir);
+    D3 color = d3(0, 0, 0);
+    if (!hit) {  // AmbientLight.Hit (ray/objects.go:68-73)
+        const double t = 0.5 * (ud.y + 1.0);
+        const D3 bg_a = d3(uni->bg_a.x, uni->bg_a.y, uni->bg_a.z), bg_b = d3(uni->bg_b.x, uni->bg_b.y, uni->bg_b.z);
+        color = mul(L.thr, add(smul(bg_a, 1.0 - t), smul(bg_b, t)));
+    } else if (!last) {
+        const double4 g = geo_at();
+        const MatRec m = mat_at();
+        const D3 point = add(L.org, smul(L.dir, closest));                             // Ray.At (ray/ray.go:23-25)
+        const D3 outward = sdiv_rcp(sub(point, d3(g.x, g.y, g.z)), m.radius, m.rinv);  // ray/objects.go:100
+        const bool front = dot(L.dir, outward) < 0;                                    // SetFaceNormal (:19-26)
+        const D3 normal = front ? outward : neg(outward);
+        bool scattered = true;
+        D3 new_dir;
+        D3 att = d3(m.albedo[0], m.albedo[1], m.albedo[2]);
+        const bool lambertian = m.type == kLambertian;
+        D3 uv = d3(0, 0, 0);
+        if (lambertian || (m.type == kMetal && m.param > 0.0)) uv = unit_vector_from(u);
+        if (lambertian) {  // ray/materials.go:13-20
+            new_dir = add(normal, uv);
+            if (near_zero(new_dir)) new_dir = normal;
+        } else if (m.type == kMetal) {  // ray/materials.go:28-37
+            D3 reflected = reflect(ud, normal);
+            if (m.param > 0.0) reflected = add(reflected, smul(uv, m.param));
+            new_dir = reflected;
+            scattered = dot(new_dir, normal) > 0;
+        } else {  // Dielectric, ray/materials.go:44-64
+            att = d3(1.0, 1.0, 1.0);
+            const double ratio = front ? m.pinv : m.param;  // 1.0/RefIdx precomputed (same bits)
+            const double cos_theta = go_min(dot(neg(ud), normal), 1.0);
+            const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
+            const bool do_reflect = ratio * sin_theta > 1.0 || reflectance(cos_theta, ratio) > u.u0;
+            new_dir = do_reflect ? reflect(ud, normal) : refract(ud, normal, ratio);
+        }
+        if (scattered) {
+            L.thr = mul(L.thr, att);
+            L.org = point;
+            L.dir = new_dir;
+            ++L.bounce;
+        } else {
+            ends = true;  // absorbed -> black
+        }
+    }
+    if (!ends) return true;
+    if (!finish_sample<kFmt, kStats>(p, L, color, st)) return false;
+    if (hit && !last) u = camera_block(uni, L.pixel, L.sample);  // absorbed: `u` was the scatter block
+    get_ray(p, uni, u, L.fx, L.fy, L.org, L.dir);
     return true;
 }
 
@@ -500,7 +594,7 @@ __device__ __forceinline__ bool end_path(const KernelParams& p, Lane& L, const D
 
 // Diagnostic build only (-DTRAY_PROFILE): per-wave s_memtime stamps around each
 // phase of the BVH loop, plus phase and active-lane counts, added into
-// stats[3..15] (the stats buffer must then hold 16 counters). Never part of a
+// stats[3..18] (the stats buffer must then hold 19 counters). Never part of a
 // timed build: the stamps' waits serialise the phases.
 #ifdef TRAY_PROFILE
 #define PROF_T0() const uint64_t prof_t0_ = __builtin_amdgcn_s_memtime()
@@ -525,32 +619,52 @@ __device__ __forceinline__ bool end_path(const KernelParams& p, Lane& L, const D
 // traverse.
 template <bool kLDS, int kFmt, bool kBVH, bool kStats>
 __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
-    extern __shared__ __attribute__((aligned(16))) double4 smem[];
+    extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
+    __attribute__((address_space(3))) Uniforms* uni_lds =
+        (__attribute__((address_space(3))) Uniforms*)reinterpret_cast<Uniforms*>(smem_all);
+    double4* smem = smem_all + kUniformsBytes / sizeof(double4);
+    if (threadIdx.x == 0) {  // scalar stores: an aggregate copy would go through scratch
+        volatile __attribute__((address_space(3))) Uniforms* u = uni_lds;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            u->cam.position[k] = p.cam.position[k];
+            u->cam.pixel00[k] = p.cam.pixel00[k];
+            u->cam.pixel_x[k] = p.cam.pixel_x[k];
+            u->cam.pixel_y[k] = p.cam.pixel_y[k];
+            u->cam.defocus_u[k] = p.cam.defocus_u[k];
+            u->cam.defocus_v[k] = p.cam.defocus_v[k];
+        }
+        u->cam.aperture = p.cam.aperture;
+        u->bg_a.x = p.bg_a.x, u->bg_a.y = p.bg_a.y, u->bg_a.z = p.bg_a.z;
+        u->bg_b.x = p.bg_b.x, u->bg_b.y = p.bg_b.y, u->bg_b.z = p.bg_b.z;
+        u->focus_time = p.focus_time;
+        u->ray_radius = p.ray_radius;
+        u->seed = p.seed;
+    }
+    const UniPtr uni = uni_lds;
     SceneView sv{p.geo, p.nodes, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
     if constexpr (kLDS) {
         if constexpr (kBVH) {
-            // [nodes: n_nodes x 32 B][bgeo: n_slots x 32 B][bmat: n_slots x 48 B][bidx: n_slots x 4 B]
+            // [nodes: n_nodes x 32 B][bgeo: n_slots x 32 B][bidx: n_slots x 4 B]; shading
+            // records (bmat) stay in global memory (L1/L2-resident, read once per hit).
             double4* lds_nodes = smem;
             double4* lds_geo = smem + p.n_nodes;
-            MatRec* lds_mat = reinterpret_cast<MatRec*>(smem + p.n_nodes + p.n_slots);
-            int32_t* lds_idx = reinterpret_cast<int32_t*>(lds_mat + p.n_slots);
+            int32_t* lds_idx = reinterpret_cast<int32_t*>(smem + p.n_nodes + p.n_slots);
             const double4* gn = reinterpret_cast<const double4*>(p.nodes);
             for (int i = threadIdx.x; i < p.n_nodes; i += blockDim.x) lds_nodes[i] = gn[i];
             for (int i = threadIdx.x; i < p.n_slots; i += blockDim.x) {
                 lds_geo[i] = p.bgeo[i];
-                lds_mat[i] = p.bmat[i];
                 lds_idx[i] = p.bidx[i];
             }
             sv.nodes = reinterpret_cast<const BvhNode*>(lds_nodes);
             sv.bgeo = lds_geo;
-            sv.bmat = lds_mat;
             sv.bidx = lds_idx;
         } else {
             for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
             sv.geo = smem;
         }
-        __syncthreads();
     }
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     Lane L;
@@ -561,7 +675,7 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
     bool exhausted = false;
 #ifdef TRAY_PROFILE
-    uint64_t prof[13] = {};
+    uint64_t prof[16] = {};
 #endif
 
     while (true) {
@@ -589,6 +703,7 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                     int32_t x, j;
                     if (decode_pixel(p, pool_next + rank, x, j)) {
                         start_pixel(p, L, x, j);
+                        get_ray(p, uni, camera_block(uni, L.pixel, 0u), L.fx, L.fy, L.org, L.dir);
                         if constexpr (kBVH) {
                             ++L.segments;
                             trav_begin(T, L.org, L.dir);
@@ -608,9 +723,8 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                 ++L.segments;
                 double closest;
                 const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
-                D3 color;
-                if (shade(p, L, best, closest, [&] { return p.geo[best]; }, [&] { return p.mat[best]; }, color))
-                    end_path<kFmt, kStats>(p, L, color, st);
+                shade_step<kFmt, kStats>(p, uni, L, best, closest, [&] { return p.geo[best]; },
+                                         [&] { return p.mat[best]; }, st);
             }
         } else {
             // Node steps for the traversing lanes.
@@ -637,7 +751,7 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                 PROF_CNT(6, 1);
                 PROF_CNT(7, __popcll(m_leaf));
                 if (state == kLeafState) {
-                    if constexpr (kStats) st.spheres += (uint32_t)(T.leaf & 7);
+                    if constexpr (kStats) st.spheres += (uint64_t)(T.leaf & 7);
                     state = trav_leaf(T, sv, L.org, L.dir);
                 }
                 PROF_ADD(2);
@@ -650,15 +764,11 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                 PROF_CNT(8, 1);
                 PROF_CNT(9, __popcll(m_shade));
                 if (state == kShadeState) {
-                    D3 color;
-                    bool more = true;
-                    if (shade(p, L, T.best, T.closest, [&] { return sv.bgeo[T.slot]; },
-                              [&] { return sv.bmat[T.slot]; }, color))
-                        more = end_path<kFmt, kStats>(p, L, color, st);
-                    if (more) {
+                    if (shade_step<kFmt, kStats>(p, uni, L, T.best, T.closest, [&] { return sv.bgeo[T.slot]; },
+                                                 [&] { return sv.bmat[T.slot]; }, st)) {
                         ++L.segments;
                         trav_begin(T, L.org, L.dir);
-                        state = kTravState;
+                        state = sv.n_nodes > 0 ? kTravState : kShadeState;
                     } else {
                         state = kIdleState;
                     }
@@ -667,9 +777,14 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
             }
         }
     }
+    if constexpr (kStats) {
+        atomicAdd(p.stats + 0, (unsigned long long)st.segments);
+        atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
+        atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
+    }
 #ifdef TRAY_PROFILE
     if (kStats && lane == 0)
-        for (int i = 0; i < 13; ++i) atomicAdd(p.stats + 3 + i, (unsigned long long)prof[i]);
+        for (int i = 0; i < 16; ++i) atomicAdd(p.stats + 3 + i, (unsigned long long)prof[i]);
 #endif
 }
 
@@ -712,11 +827,10 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    const size_t lds_bytes = use_bvh ? (size_t)p.n_nodes * sizeof(BvhNode) +
-                                           (size_t)p.n_slots * (sizeof(double4) + sizeof(MatRec) + 4)
+    const size_t lds_bytes = use_bvh ? (size_t)p.n_nodes * sizeof(BvhNode) + (size_t)p.n_slots * (sizeof(double4) + 4)
                                      : (size_t)p.n_pad * sizeof(double4);
-    const bool use_lds = lds_bytes <= kMaxLDSBytes;
-    const size_t lds = use_lds ? (lds_bytes + 15) / 16 * 16 : 0;
+    const bool use_lds = lds_bytes + kUniformsBytes <= kMaxLDSBytes;
+    const size_t lds = kUniformsBytes + (use_lds ? (lds_bytes + 15) / 16 * 16 : 0);
     const bool stats = p.stats != nullptr;
     const KernelFn fn = pick_kernel(use_lds, use_bvh, stats, p.out_format);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
@@ -748,7 +862,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (e != hipSuccess) return e;
     if (stats) {
 #ifdef TRAY_PROFILE
-        e = hipMemsetAsync(p.stats, 0, 16 * sizeof(unsigned long long), stream);
+        e = hipMemsetAsync(p.stats, 0, 19 * sizeof(unsigned long long), stream);
 #else
         e = hipMemsetAsync(p.stats, 0, 3 * sizeof(unsigned long long), stream);
 #endif

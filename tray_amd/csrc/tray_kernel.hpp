@@ -18,11 +18,13 @@ enum : int32_t { kOutRGBF64 = 0, kOutRGBF32 = 1, kOutRGBA8 = 2 };
 // read the same array from global memory (L2/L1-resident).
 constexpr size_t kMaxLDSBytes = 160 * 1024;
 
-// Per-sphere shading record, read only for the closest hit (48 B).
+// Per-sphere shading record, read only for the closest hit (64 B).
 struct MatRec {
     double albedo[3];
     double param;   // Metal.Fuzz / Dielectric.RefIdx
     double radius;  // Sphere.Radius (normal = (P - C) / R, ray/objects.go:100)
+    double rinv;    // RN(1 / Radius): exact quotients via div_rcp (tray_kernel.hip)
+    double pinv;    // RN(1 / RefIdx) = Go's 1.0/d.RefIdx (ray/materials.go:48)
     int32_t type;
     int32_t pad;
 };
