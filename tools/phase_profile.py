@@ -10,7 +10,7 @@ import json
 import os
 import sys
 
-PHASES = ("cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade", "cyc_gen")
+PHASES = ("cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--config", default="c2")
+    ap.add_argument("--waves", type=int, default=256 * 16, help="waves in the launch (CUs x waves per CU)")
     args = ap.parse_args()
     import torch
 
@@ -32,13 +33,16 @@ def main():
     scene = _lib.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0, os.path.abspath(args.lib))
     params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
     out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-    stats = torch.zeros(19, dtype=torch.int64, device="cuda")
+    stats = torch.zeros(32 + 2 * args.waves, dtype=torch.int64, device="cuda")
     scene.render_stats_async(cam._state, params, out.data_ptr(), stats.data_ptr(),
                              torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    v = stats.tolist()
+    allv = stats.tolist()
+    v = allv[:19]
+    se = allv[32:]
     names = ["segments", "sphere_tests", "box_tests", "cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade",
-             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "gen_phases", "gen_lanes", "cyc_gen"]
+             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "unused_11", "unused_12", "rt_end_max", "rt_life_sum",
+             "rt_start_min_inv"]
     d = dict(zip(names, v))
     cyc = sum(d[k] for k in PHASES)
     d["share"] = {k: round(d[k] / cyc, 3) for k in PHASES}
@@ -48,8 +52,23 @@ def main():
     d["cyc_per_node_iter"] = round(d["cyc_node"] / max(1, d["node_iters"]), 1)
     d["cyc_per_leaf_phase"] = round(d["cyc_leaf"] / max(1, d["leaf_phases"]), 1)
     d["cyc_per_shade_phase"] = round(d["cyc_shade"] / max(1, d["shade_phases"]), 1)
-    d["lanes_per_gen_phase"] = round(d["gen_lanes"] / max(1, d["gen_phases"]), 1)
-    d["cyc_per_gen_phase"] = round(d["cyc_gen"] / max(1, d["gen_phases"]), 1)
+    # Tail: kernel span (latest exit - earliest start) vs the mean wave lifetime,
+    # on the 100 MHz constant-rate clock (s_memrealtime).
+    start_min = (1 << 64) - 1 - (d["rt_start_min_inv"] % (1 << 64))
+    waves = args.waves
+    span = d["rt_end_max"] - start_min
+    d["span_us"] = round(span / 100.0, 1)
+    d["mean_wave_life_us"] = round(d["rt_life_sum"] / waves / 100.0, 1)
+    d["tail_idle_frac"] = round(1.0 - d["rt_life_sum"] / waves / max(1, span), 4)
+    import numpy as np
+    st_ = np.array(se[0::2], dtype=np.float64)
+    en_ = np.array(se[1::2], dtype=np.float64)
+    ok = en_ > 0
+    st_, en_ = st_[ok] - start_min, en_[ok] - start_min
+    q = [0, 1, 10, 50, 90, 99, 100]
+    d["waves_seen"] = int(ok.sum())
+    d["wave_start_us_pct"] = {str(k): round(float(np.percentile(st_, k)) / 100.0, 1) for k in q}
+    d["wave_end_us_pct"] = {str(k): round(float(np.percentile(en_, k)) / 100.0, 1) for k in q}
     print(json.dumps(d))
 
 

@@ -102,11 +102,15 @@ struct tray_scene_s {
     // exact-culling BVH (absent for tiny or non-finite scenes)
     bool has_bvh;
     double bvh_bound;
-    int32_t n_nodes, n_slots;
-    tray::BvhNode* nodes;
+    int32_t n_nodes, n_slots, stack_cap;
+    tray::Bvh4Node* nodes;
     double4* bgeo;
     int32_t* bidx;
     tray::MatRec* bmat;
+    // Per-sample path colours of one launch band (tray_kernel.hpp), grown on
+    // demand: renders of one scene must be ordered (one stream, or synchronised).
+    double* samples;
+    size_t samples_bytes;
 };
 
 using namespace tray;
@@ -209,12 +213,22 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         m.type = s.material;
         m.pad = 0;
     }
+    // One sphere per leaf unless the scene then no longer fits the CU's LDS,
+    // where a few spheres per leaf (fewer nodes) may still fit it.
     Bvh bvh;
-    const bool has_bvh = n >= kBvhMinSpheres && build_bvh(spheres, n, &bvh);
-    if (has_bvh) {  // kBvhLeafMax NaN slots so a leaf read of kBvhLeafMax spheres stays in bounds
-        for (int k = 0; k < kBvhLeafMax; ++k) {
-            bvh.geo.push_back(make_double4(qnan, qnan, qnan, qnan));
-            bvh.idx.push_back(0x7fffffff);
+    bool has_bvh = false;
+    if (n >= kBvhMinSpheres) {
+        for (int leaf_max = 1; leaf_max <= kBvhLeafMax; leaf_max *= 2) {
+            Bvh b;
+            if (!build_bvh(spheres, n, &b, leaf_max)) continue;
+            const int32_t cap = b.stack_max + 1;  // + the scratch slot (tray_kernel.hip Stack)
+            if (bvh_scene_lds_bytes(0, 0, cap) > kMaxLDSBytes) continue;  // stack alone too deep
+            const bool fits = bvh_scene_lds_bytes((int32_t)b.nodes.size(), (int32_t)b.geo.size(), cap) <= kMaxLDSBytes;
+            if (!has_bvh || fits) {
+                bvh = std::move(b);
+                has_bvh = true;
+            }
+            if (fits) break;
         }
     }
     tray_scene_s* sc = new tray_scene_s();
@@ -223,10 +237,13 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->bvh_bound = bvh.bound;
     sc->n_nodes = (int32_t)bvh.nodes.size();
     sc->n_slots = (int32_t)bvh.geo.size();
+    sc->stack_cap = bvh.stack_max + 1;
     sc->nodes = nullptr;
     sc->bgeo = nullptr;
     sc->bidx = nullptr;
     sc->bmat = nullptr;
+    sc->samples = nullptr;
+    sc->samples_bytes = 0;
     std::vector<MatRec> bmat(bvh.idx.size());
     for (size_t i = 0; i < bvh.idx.size(); ++i) {
         const int32_t k = bvh.idx[i];
@@ -246,11 +263,11 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     if (e == hipSuccess && n > 0) e = hipMalloc(&sc->mat, sizeof(MatRec) * (size_t)n);
     if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess && has_bvh) {
-        e = hipMalloc(&sc->nodes, sizeof(BvhNode) * bvh.nodes.size());
+        e = hipMalloc(&sc->nodes, sizeof(Bvh4Node) * bvh.nodes.size());
         if (e == hipSuccess) e = hipMalloc(&sc->bgeo, sizeof(double4) * bvh.geo.size());
         if (e == hipSuccess) e = hipMalloc(&sc->bidx, sizeof(int32_t) * bvh.idx.size());
         if (e == hipSuccess)
-            e = hipMemcpy(sc->nodes, bvh.nodes.data(), sizeof(BvhNode) * bvh.nodes.size(), hipMemcpyHostToDevice);
+            e = hipMemcpy(sc->nodes, bvh.nodes.data(), sizeof(Bvh4Node) * bvh.nodes.size(), hipMemcpyHostToDevice);
         if (e == hipSuccess)
             e = hipMemcpy(sc->bgeo, bvh.geo.data(), sizeof(double4) * bvh.geo.size(), hipMemcpyHostToDevice);
         if (e == hipSuccess)
@@ -284,6 +301,7 @@ int tray_scene_release(tray_scene_t sc) {
     if (sc->bgeo) (void)hipFree(sc->bgeo);
     if (sc->bidx) (void)hipFree(sc->bidx);
     if (sc->bmat) (void)hipFree(sc->bmat);
+    if (sc->samples) (void)hipFree(sc->samples);
     delete sc;
     return TRAY_OK;
 }
@@ -331,6 +349,7 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.bmat = sc->bmat;
     k.n_nodes = sc->n_nodes;
     k.n_slots = sc->n_slots;
+    k.stack_cap = sc->stack_cap;
     // The BVH's conservative FP32 box test assumes every ray origin lies within
     // [-M, M]^3 (tray_bvh.cpp): hit points do; check the camera and lens disc.
     double cam_extent = 0;
@@ -339,6 +358,20 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
                   std::fabs(cam->defocus_v[0]) + std::fabs(cam->defocus_v[1]) + std::fabs(cam->defocus_v[2]);
     const bool use_bvh = sc->has_bvh && !(p->flags & TRAY_FLAG_LINEAR_SCAN) && cam_extent <= sc->bvh_bound;
     TRAY_HIP(hipSetDevice(sc->device));
+    if (!band_fits(p->width, p->rays_per_pixel))
+        return fail(TRAY_ERR_TOO_LARGE, "width x rays_per_pixel too large (8 rows of samples exceed 2^31)");
+    const size_t need = sample_buffer_bytes(p->width, k.rows, p->rays_per_pixel);
+    if (need > sc->samples_bytes) {
+        if (sc->samples) {
+            TRAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+            TRAY_HIP(hipFree(sc->samples));
+            sc->samples = nullptr;
+            sc->samples_bytes = 0;
+        }
+        TRAY_HIP(hipMalloc(&sc->samples, need));
+        sc->samples_bytes = need;
+    }
+    k.samples = sc->samples;
     TRAY_HIP(launch_render(k, use_bvh, static_cast<hipStream_t>(stream)));
     return TRAY_OK;
 }

@@ -16,6 +16,10 @@
 // exact interval of the unpadded sphere box. The kernel requires every ray
 // origin to satisfy |o| <= M (hit points lie inside the boxes; the camera is
 // checked at launch, else the linear scan is used).
+//
+// Build: binned SAH over sphere centroids into a binary tree (object-median
+// splits once a branch gets deep, so depth stays bounded), then collapsed into
+// 4-wide nodes by repeatedly opening the largest-area inner child.
 
 #include <math.h>
 #include <stdint.h>
@@ -53,13 +57,25 @@ struct Prim {
     int32_t index;
 };
 
+// Binary node: leaf when count > 0 (prims [first, first + count)).
+struct Node2 {
+    Box box;
+    int32_t left = -1, right = -1;
+    int32_t first = 0, count = 0;
+};
+
+// Past this depth splits are object medians: depth <= kSahDepth + log2(n).
+constexpr int kSahDepth = 32;
+
 struct Builder {
     std::vector<Prim> prims;
-    std::vector<BvhNode> nodes;
+    std::vector<Node2> bin;
+    std::vector<Bvh4Node> nodes;
     std::vector<double4> geo;
     std::vector<int32_t> idx;
     double pad = 0;
-    int leaf_max = kBvhLeafMax;
+    int leaf_max = 1;
+    int32_t stack_max = 0;
 
     static float down(double v) {
         float f = (float)v;
@@ -72,38 +88,27 @@ struct Builder {
         return f;
     }
 
-    // Emit the subtree over prims[b, e) in depth-first order; returns node index.
-    int build(int b, int e, const tray_sphere* s) {
+    int build2(int b, int e, int depth) {
+        const int me = (int)bin.size();
+        bin.push_back(Node2{});
         Box box;
         for (int i = b; i < e; ++i) box.grow(prims[i].box);
-        const int me = (int)nodes.size();
-        nodes.push_back(BvhNode{});
-        for (int k = 0; k < 3; ++k) {
-            nodes[me].lo[k] = down(box.lo[k] - pad);
-            nodes[me].hi[k] = up(box.hi[k] + pad);
-        }
-        const int count = e - b;
-        if (count <= leaf_max) {
-            const int slot = (int)geo.size();
-            for (int i = b; i < e; ++i) {
-                const tray_sphere& sp = s[prims[i].index];
-                geo.push_back(make_double4(sp.center[0], sp.center[1], sp.center[2], sp.radius * sp.radius));
-                idx.push_back(prims[i].index);
-            }
-            nodes[me].leaf = (slot << 3) | count;
-            nodes[me].skip = me + 1;
+        bin[me].box = box;
+        if (e - b <= leaf_max) {
+            bin[me].first = b;
+            bin[me].count = e - b;
             return me;
         }
-        const int mid = split(b, e, box);
-        build(b, mid, s);
-        build(mid, e, s);
-        nodes[me].leaf = -1;
-        nodes[me].skip = (int)nodes.size();
+        const int mid = split(b, e, depth);
+        const int l = build2(b, mid, depth + 1);
+        const int r = build2(mid, e, depth + 1);
+        bin[me].left = l;
+        bin[me].right = r;
         return me;
     }
 
-    // Binned SAH over centroids; falls back to a median split on degenerate input.
-    int split(int b, int e, const Box& box) {
+    // Binned SAH over centroids; object median when deep or degenerate.
+    int split(int b, int e, int depth) {
         constexpr int kBins = 32;
         double cmin[3], cmax[3];
         for (int k = 0; k < 3; ++k) {
@@ -117,7 +122,7 @@ struct Builder {
             }
         double best_cost = INFINITY;
         int best_axis = -1, best_bin = -1;
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < 3 && depth < kSahDepth; ++k) {
             const double ext = cmax[k] - cmin[k];
             if (!(ext > 0)) continue;
             Box bins[kBins];
@@ -152,7 +157,7 @@ struct Builder {
                 }
             }
         }
-        int mid;
+        int mid = b;
         if (best_axis >= 0) {
             const int k = best_axis;
             const double ext = cmax[k] - cmin[k];
@@ -162,16 +167,74 @@ struct Builder {
                 return bi <= best_bin;
             });
             mid = (int)(m - prims.data());
-        } else {
-            mid = b;
         }
-        if (mid <= b || mid >= e) {  // all centroids equal: split by list position
+        if (mid <= b || mid >= e) {  // median along the widest centroid extent (ties: list order)
+            int k = 0;
+            for (int a = 1; a < 3; ++a)
+                if (cmax[a] - cmin[a] > cmax[k] - cmin[k]) k = a;
             mid = b + (e - b) / 2;
+            std::nth_element(prims.begin() + b, prims.begin() + mid, prims.begin() + e, [k](const Prim& x, const Prim& y) {
+                return x.c[k] < y.c[k] || (x.c[k] == y.c[k] && x.index < y.index);
+            });
         }
         // Keep each side's primitives in list order (deterministic, index-ordered leaves).
         std::sort(prims.begin() + b, prims.begin() + mid, [](const Prim& x, const Prim& y) { return x.index < y.index; });
         std::sort(prims.begin() + mid, prims.begin() + e, [](const Prim& x, const Prim& y) { return x.index < y.index; });
         return mid;
+    }
+
+    // Emit the 4-wide node for binary inner node `n` (pre-order); `depth_stack`
+    // = stack entries its ancestors may have left. Returns the node index.
+    int collapse(int n, int32_t depth_stack, const tray_sphere* s) {
+        int ch[kBvhWidth] = {bin[n].left, bin[n].right, -1, -1};
+        int cnt = 2;
+        while (cnt < kBvhWidth) {  // open the largest-area inner child
+            int pick = -1;
+            double pick_area = -1;
+            for (int k = 0; k < cnt; ++k)
+                if (bin[ch[k]].count == 0 && bin[ch[k]].box.area() > pick_area) {
+                    pick = k;
+                    pick_area = bin[ch[k]].box.area();
+                }
+            if (pick < 0) break;
+            const int c = ch[pick];
+            ch[pick] = bin[c].left;
+            ch[cnt++] = bin[c].right;
+        }
+        const int me = (int)nodes.size();
+        nodes.push_back(Bvh4Node{});
+        int inner = 0;
+        for (int k = 0; k < cnt; ++k) inner += bin[ch[k]].count == 0;
+        const int32_t here = depth_stack + std::max(inner - 1, 0);
+        stack_max = std::max(stack_max, here);
+        for (int k = 0; k < kBvhWidth; ++k) {
+            if (k >= cnt) {
+                for (int a = 0; a < 3; ++a) {
+                    nodes[me].box[a][0][k] = INFINITY;
+                    nodes[me].box[a][1][k] = -INFINITY;
+                }
+                nodes[me].child[k] = kBvhEmpty;
+                continue;
+            }
+            const Node2& c = bin[ch[k]];
+            for (int a = 0; a < 3; ++a) {
+                nodes[me].box[a][0][k] = down(c.box.lo[a] - pad);
+                nodes[me].box[a][1][k] = up(c.box.hi[a] + pad);
+            }
+            if (c.count > 0) {
+                const int slot = (int)geo.size();
+                for (int i = c.first; i < c.first + c.count; ++i) {
+                    const tray_sphere& sp = s[prims[i].index];
+                    geo.push_back(make_double4(sp.center[0], sp.center[1], sp.center[2], sp.radius * sp.radius));
+                    idx.push_back(prims[i].index);
+                }
+                nodes[me].child[k] = ~((slot << 3) | c.count);
+            } else {
+                const int sub = collapse(ch[k], here, s);
+                nodes[me].child[k] = sub;
+            }
+        }
+        return me;
     }
 };
 
@@ -182,6 +245,7 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     out->geo.clear();
     out->idx.clear();
     out->bound = 0;
+    out->stack_max = 0;
     if (n <= 0) return true;
     Builder B;
     B.prims.resize((size_t)n);
@@ -201,11 +265,17 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     m = std::max(m, 1.0);
     B.pad = 4e-6 * m;
     B.leaf_max = std::min(std::max(leaf_max, 1), kBvhLeafMax);
-    out->bound = m;
-    B.build(0, n, s);
+    if (n <= B.leaf_max) return false;  // root must be an inner node
+    B.bin.reserve((size_t)2 * n);
+    const int root = B.build2(0, n, 0);
+    B.collapse(root, 0, s);
+    if ((int64_t)B.nodes.size() > kBvhMaxNodes) return false;
     out->nodes.swap(B.nodes);
     out->geo.swap(B.geo);
     out->idx.swap(B.idx);
+    out->bound = m;
+    out->stack_max = B.stack_max;
+    out->leaf_max = B.leaf_max;
     return true;
 }
 

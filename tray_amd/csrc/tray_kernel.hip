@@ -205,35 +205,13 @@ __device__ __forceinline__ int32_t row_of(const KernelParams& p, int32_t j) {
 // Per-lane path state. A lane owns one pixel at a time and walks its samples
 // in order; when the last sample ends it writes the pixel and takes another.
 struct Lane {
-    D3 org, dir, thr, sum;
-    uint32_t pixel, sample, bounce, segments;
-    int32_t x, j;  // image column, compact output row
-    double fx, fy;
+    D3 org, dir, thr;
+    uint32_t item;                              // work item (sample) index in the band
+    uint32_t pixel, sample, bounce, segments;  // segments of this path
+    int32_t x, j;                               // image column, compact output row
     bool busy;
 };
 
-template <int kFmt>
-__device__ __forceinline__ void write_pixel(const KernelParams& p, const Lane& L) {
-    const double inv = 1.0 / (double)p.spp;  // colorSumDiv (ray/tracer.go:123)
-    const D3 mean = smul(L.sum, inv);
-    const size_t off = (size_t)L.j * (size_t)p.width + (size_t)L.x;
-    if constexpr (kFmt == kOutRGBF64) {
-        double* o = static_cast<double*>(p.out) + off * 3;
-        o[0] = mean.x;
-        o[1] = mean.y;
-        o[2] = mean.z;
-    } else if constexpr (kFmt == kOutRGBF32) {
-        float* o = static_cast<float*>(p.out) + off * 3;
-        o[0] = (float)mean.x;
-        o[1] = (float)mean.y;
-        o[2] = (float)mean.z;
-    } else {
-        const uint32_t rgba = linear_to_srgb(mean.x) | (linear_to_srgb(mean.y) << 8) |
-                              (linear_to_srgb(mean.z) << 16) | (255u << 24);
-        static_cast<uint32_t*>(p.out)[off] = rgba;
-    }
-    if (p.segments) p.segments[off] = L.segments;
-}
 
 // Candidate root of one sphere whose discriminant is >= 0 (Sphere.Hit,
 // ray/objects.go:86-94): the first root inside (1e-6, closest) wins. Used by the
@@ -297,8 +275,8 @@ struct Stats {
 // scene does not fit).
 struct SceneView {
     const double4* geo;     // linear scan: list order, NaN-padded
-    const BvhNode* nodes;   // BVH: depth-first nodes
-    const double4* bgeo;    // BVH: spheres in leaf-slot order (+4 NaN slots)
+    const Bvh4Node* nodes;  // BVH: 4-wide nodes, root first
+    const double4* bgeo;    // BVH: spheres in leaf-slot order
     const int32_t* bidx;    // BVH: original list index of each slot
     const MatRec* bmat;     // BVH: shading record of each slot
     int32_t n, n_nodes;
@@ -340,20 +318,33 @@ __device__ __forceinline__ float f32_up(double v) {
     return f;
 }
 
-// Per-lane traversal state of one Scene.Hit through the exact-culling BVH
-// (tray_bvh.cpp): stackless depth-first walk with skip links, conservative FP32
-// slab tests on padded boxes (culled against the current closest hit), FP64
-// sphere tests with the reference's arithmetic and the any-order acceptance rule.
+// Per-lane traversal state of one Scene.Hit through the exact-culling 4-wide
+// BVH (tray_bvh.cpp): conservative FP32 slab tests of a node's four child boxes
+// (culled against the current closest hit), near-first descent with a per-lane
+// stack in LDS, FP64 sphere tests with the reference's arithmetic and the
+// any-order acceptance rule.
 // Lane states of the BVH kernel.
 enum : uint32_t { kIdleState = 0, kTravState = 1, kLeafState = 2, kShadeState = 3 };
 
 struct Trav {
     float ix, iy, iz, oix, oiy, oiz;  // FP32 ray: t = box * inv - org * inv
     float tlim;                       // closest rounded up to float
-    int32_t node, leaf;
+    int32_t near_x, near_y, near_z;   // byte offsets of the near planes in a node
+    int32_t node;                     // inner node to visit next, -1: none
+    int32_t pend;                     // node whose hit leaf children wait for the leaf phase
+    uint32_t pmask;                   // ... and which of its children they are
+    int32_t sp, top;                  // stack depth; its top entry (the rest is in LDS)
     double a, a_inv, closest;
     int32_t best;  // original list index of the closest hit (tie-break key)
-    int32_t slot;  // its leaf slot (LDS-resident geometry + shading record)
+    int32_t slot;  // its leaf slot (geometry + shading record)
+};
+
+// Per-lane traversal stack: 16-bit node indices in LDS, slot i of the lane at
+// base[i * blockDim.x] (consecutive lanes, consecutive banks). The top entry
+// lives in Trav::top and slot i >= 1 holds the entry below the i-th; slot 0 is
+// a scratch slot, so pushes and pops need no branches (stack_cap = depth + 1).
+struct Stack {
+    __attribute__((address_space(3))) uint16_t* base;  // this lane's slot 0
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir) {
@@ -364,7 +355,9 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
     T.slot = 0;
     T.tlim = __builtin_inff();
     T.node = 0;
-    T.leaf = -1;
+    T.pmask = 0;
+    T.sp = 0;
+    T.top = 0;
     float dxf = (float)dir.x, dyf = (float)dir.y, dzf = (float)dir.z;
     if (__builtin_fabsf(dxf) < 1e-30f) dxf = 1e-30f;
     if (__builtin_fabsf(dyf) < 1e-30f) dyf = 1e-30f;
@@ -376,143 +369,196 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
     T.oix = (float)org.x * T.ix;
     T.oiy = (float)org.y * T.iy;
     T.oiz = (float)org.z * T.iz;
+    // Bvh4Node::box[a][s]: the near plane is the low one when the ray runs up the axis.
+    T.near_x = T.ix < 0.0f ? 16 : 0;
+    T.near_y = T.iy < 0.0f ? 48 : 32;
+    T.near_z = T.iz < 0.0f ? 80 : 64;
 }
 
-// One node visit. Returns the new lane state: kTrav, kLeaf (holds T.leaf) or
-// kShade (traversal finished).
-__device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv) {
-    const uint4* np = reinterpret_cast<const uint4*>(sv.nodes + T.node);
-    const uint4 q0 = np[0], q1 = np[1];
-    const float lox = __uint_as_float(q0.x), loy = __uint_as_float(q0.y), loz = __uint_as_float(q0.z);
-    const float hix = __uint_as_float(q0.w), hiy = __uint_as_float(q1.x), hiz = __uint_as_float(q1.y);
-    const int32_t skip = (int32_t)q1.z, leaf = (int32_t)q1.w;
-    const float t0x = __builtin_fmaf(lox, T.ix, -T.oix), t1x = __builtin_fmaf(hix, T.ix, -T.oix);
-    const float t0y = __builtin_fmaf(loy, T.iy, -T.oiy), t1y = __builtin_fmaf(hiy, T.iy, -T.oiy);
-    const float t0z = __builtin_fmaf(loz, T.iz, -T.oiz), t1z = __builtin_fmaf(hiz, T.iz, -T.oiz);
-    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
-                                     __builtin_fmaxf(__builtin_fminf(t0z, t1z), 0.0f));
-    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
-                                     __builtin_fminf(__builtin_fmaxf(t0z, t1z), T.tlim));
-    const bool hit = tn <= tf;
-    T.node = (hit && leaf < 0) ? T.node + 1 : skip;
-    if (hit && leaf >= 0) {
-        T.leaf = leaf;
+// Push the node in sort key `key` if the key is valid. The store is
+// unconditional: with no push it writes slot sp, above the stack.
+__device__ __forceinline__ void stack_push(Trav& T, const Stack& S, uint32_t key) {
+    const bool valid = key != ~0u;
+    S.base[T.sp * (int32_t)blockDim.x] = (uint16_t)T.top;
+    T.top = valid ? (int32_t)(key & 0xFFFFu) : T.top;
+    T.sp += valid ? 1 : 0;
+}
+
+// 1: slab distances of two children per packed FMA (v_pk_fma_f32).
+#ifndef TRAY_PK_FMA
+#define TRAY_PK_FMA 0
+#endif
+
+// One node visit: test the four child boxes; hit leaf children are handed to
+// the leaf phase, the nearest hit inner child is visited next and the other hit
+// inner children are pushed far-to-near. Returns the new lane state.
+__device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, const Stack& S, uint32_t& tested) {
+    const char* nb = reinterpret_cast<const char*>(sv.nodes + T.node);
+    // Near and far planes of the four children on each axis (far = near ^ 16).
+    const float4 nx = *reinterpret_cast<const float4*>(nb + T.near_x);
+    const float4 fx = *reinterpret_cast<const float4*>(nb + (T.near_x ^ 16));
+    const float4 ny = *reinterpret_cast<const float4*>(nb + T.near_y);
+    const float4 fy = *reinterpret_cast<const float4*>(nb + (T.near_y ^ 16));
+    const float4 nz = *reinterpret_cast<const float4*>(nb + T.near_z);
+    const float4 fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ 16));
+    const int4 ch = *reinterpret_cast<const int4*>(nb + 96);
+    // Entry below the top, read ahead for a pop (slot max(sp - 1, 0)).
+    const int32_t below = (int32_t)S.base[max(T.sp - 1, 0) * (int32_t)blockDim.x];
+    const int32_t child[4] = {ch.x, ch.y, ch.z, ch.w};
+#if TRAY_PK_FMA
+    typedef float tray_f2 __attribute__((ext_vector_type(2)));
+    // Slab distances, two children per packed FMA: t = plane * inv - org * inv.
+    const tray_f2 ixv = {T.ix, T.ix}, iyv = {T.iy, T.iy}, izv = {T.iz, T.iz};
+    const tray_f2 oxv = {-T.oix, -T.oix}, oyv = {-T.oiy, -T.oiy}, ozv = {-T.oiz, -T.oiz};
+    const tray_f2 tnx01 = __builtin_elementwise_fma(tray_f2{nx.x, nx.y}, ixv, oxv), tnx23 = __builtin_elementwise_fma(tray_f2{nx.z, nx.w}, ixv, oxv);
+    const tray_f2 tfx01 = __builtin_elementwise_fma(tray_f2{fx.x, fx.y}, ixv, oxv), tfx23 = __builtin_elementwise_fma(tray_f2{fx.z, fx.w}, ixv, oxv);
+    const tray_f2 tny01 = __builtin_elementwise_fma(tray_f2{ny.x, ny.y}, iyv, oyv), tny23 = __builtin_elementwise_fma(tray_f2{ny.z, ny.w}, iyv, oyv);
+    const tray_f2 tfy01 = __builtin_elementwise_fma(tray_f2{fy.x, fy.y}, iyv, oyv), tfy23 = __builtin_elementwise_fma(tray_f2{fy.z, fy.w}, iyv, oyv);
+    const tray_f2 tnz01 = __builtin_elementwise_fma(tray_f2{nz.x, nz.y}, izv, ozv), tnz23 = __builtin_elementwise_fma(tray_f2{nz.z, nz.w}, izv, ozv);
+    const tray_f2 tfz01 = __builtin_elementwise_fma(tray_f2{fz.x, fz.y}, izv, ozv), tfz23 = __builtin_elementwise_fma(tray_f2{fz.z, fz.w}, izv, ozv);
+    const float tnx[4] = {tnx01.x, tnx01.y, tnx23.x, tnx23.y}, tfx[4] = {tfx01.x, tfx01.y, tfx23.x, tfx23.y};
+    const float tny[4] = {tny01.x, tny01.y, tny23.x, tny23.y}, tfy[4] = {tfy01.x, tfy01.y, tfy23.x, tfy23.y};
+    const float tnz[4] = {tnz01.x, tnz01.y, tnz23.x, tnz23.y}, tfz[4] = {tfz01.x, tfz01.y, tfz23.x, tfz23.y};
+#else
+    // Slab distances: t = plane * inv - org * inv.
+    const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
+    const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
+    const float nza[4] = {nz.x, nz.y, nz.z, nz.w}, fza[4] = {fz.x, fz.y, fz.z, fz.w};
+    float tnx[4], tfx[4], tny[4], tfy[4], tnz[4], tfz[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        tnx[k] = __builtin_fmaf(nxa[k], T.ix, -T.oix);
+        tfx[k] = __builtin_fmaf(fxa[k], T.ix, -T.oix);
+        tny[k] = __builtin_fmaf(nya[k], T.iy, -T.oiy);
+        tfy[k] = __builtin_fmaf(fya[k], T.iy, -T.oiy);
+        tnz[k] = __builtin_fmaf(nza[k], T.iz, -T.oiz);
+        tfz[k] = __builtin_fmaf(fza[k], T.iz, -T.oiz);
+    }
+#endif
+    // Hit inner children: upper 16 bits of the entry distance | node index (tn >= 0,
+    // so the keys order like the distances, to bf16 precision); anything else ~0.
+    // An empty child's planes are (+inf, -inf): tn = +inf, never a hit.
+    uint32_t key[4];
+    uint32_t leaves = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx[k], tny[k]), tnz[k]), 0.0f);
+        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fminf(tfx[k], tfy[k]), tfz[k]), T.tlim);
+        const uint32_t hit = (uint32_t)(tn <= tf);
+        const uint32_t inner = (uint32_t)(child[k] >= 0);
+        const uint32_t keep = 0u - (hit & inner);  // all ones iff a hit inner child
+        key[k] = (((__float_as_uint(tn) & 0xFFFF0000u) | (uint32_t)child[k]) & keep) | ~keep;
+        leaves |= (hit & (inner ^ 1u)) << k;
+    }
+    tested = (uint32_t)(child[0] != kBvhEmpty) + (uint32_t)(child[1] != kBvhEmpty) +
+             (uint32_t)(child[2] != kBvhEmpty) + (uint32_t)(child[3] != kBvhEmpty);
+#define TRAY_CX(i, j)                             \
+    {                                             \
+        const uint32_t lo_ = min(key[i], key[j]); \
+        key[j] = max(key[i], key[j]);             \
+        key[i] = lo_;                             \
+    }
+    TRAY_CX(0, 1) TRAY_CX(2, 3) TRAY_CX(0, 2) TRAY_CX(1, 3) TRAY_CX(1, 2)
+#undef TRAY_CX
+    stack_push(T, S, key[3]);
+    stack_push(T, S, key[2]);
+    stack_push(T, S, key[1]);
+    const int32_t here = T.node;
+    const bool has = key[0] != ~0u;
+    const bool pop = !has && T.sp > 0;
+    T.node = has ? (int32_t)(key[0] & 0xFFFFu) : pop ? T.top : -1;
+    T.top = pop ? below : T.top;
+    T.sp -= pop ? 1 : 0;
+    if (leaves != 0u) {
+        T.pend = here;
+        T.pmask = leaves;
         return kLeafState;
     }
-    return T.node < sv.n_nodes ? kTravState : kShadeState;
+    return T.node >= 0 ? kTravState : kShadeState;
 }
 
-#ifndef TRAY_LEAF_COMPACT
-#define TRAY_LEAF_COMPACT 1
-#endif
-// Test the held leaf's <= kBvhLeafMax spheres (FP64, any-order rule).
-__device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const D3& org, const D3& dir) {
-    const int slot = T.leaf >> 3, cnt = T.leaf & 7;
-    double h[kBvhLeafMax], d[kBvhLeafMax];
-#pragma unroll
-    for (int k = 0; k < kBvhLeafMax; ++k) {
-        quad(sv.bgeo[slot + k], org, dir, T.a, h[k], d[k]);
-        if (k >= cnt) d[k] = __builtin_nan("");
-    }
-#if TRAY_LEAF_COMPACT
-    // Only spheres whose discriminant is >= 0 need the root (a sqrt and two
-    // divisions): each lane walks its own candidates, so the wave pays for
-    // max-over-lanes(candidates) roots instead of kBvhLeafMax.
-    uint32_t cand = 0;
-#pragma unroll
-    for (int k = 0; k < kBvhLeafMax; ++k) cand |= (d[k] >= 0) ? (1u << k) : 0u;
-    if (cand != 0u) {
-        while (cand != 0u) {
-            const int k = __builtin_ctz(cand);
-            cand &= cand - 1u;
-            double hk = h[0], dk = d[0];
-#pragma unroll
-            for (int q = 1; q < kBvhLeafMax; ++q) {
-                hk = k == q ? h[q] : hk;
-                dk = k == q ? d[q] : dk;
+// Test the pending leaf children's spheres (FP64, any-order rule). Each lane
+// walks its own leaves, so the wave pays for max-over-lanes(spheres) tests.
+__device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const D3& org, const D3& dir,
+                                              uint32_t& tested) {
+    const int4 ch = reinterpret_cast<const int4*>(sv.nodes + T.pend)[6];
+    uint32_t m = T.pmask;
+    tested = 0;
+    while (m != 0u) {
+        const uint32_t k = (uint32_t)__builtin_ctz(m);
+        m &= m - 1u;
+        const int32_t ref = ~(k == 0u ? ch.x : k == 1u ? ch.y : k == 2u ? ch.z : ch.w);
+        const int32_t first = ref >> 3, end = first + (ref & 7);
+        for (int32_t slot = first; slot < end; ++slot) {
+            double h, d;
+            quad(sv.bgeo[slot], org, dir, T.a, h, d);
+            if (d >= 0) {
+                const int32_t before = T.best;
+                candidate_any_order(h, d, T.a, T.a_inv, sv.bidx[slot], T.closest, T.best);
+                if (T.best != before) T.slot = slot;
             }
-            const int32_t idx = sv.bidx[slot + k];
-            const int32_t before = T.best;
-            candidate_any_order(hk, dk, T.a, T.a_inv, idx, T.closest, T.best);
-            if (T.best != before) T.slot = slot + k;
+            ++tested;
         }
-        T.tlim = f32_up(T.closest);
     }
-#else
-    double m = d[0];
-#pragma unroll
-    for (int k = 1; k < kBvhLeafMax; ++k) m = __builtin_fmax(m, d[k]);
-    if (m >= 0) {
-#pragma unroll
-        for (int k = 0; k < kBvhLeafMax; ++k) {
-            const int32_t idx = sv.bidx[slot + k];
-            const int32_t before = T.best;
-            candidate_any_order(h[k], d[k], T.a, T.a_inv, idx, T.closest, T.best);
-            if (T.best != before) T.slot = slot + k;
-        }
-        T.tlim = f32_up(T.closest);
-    }
-#endif
-    T.leaf = -1;
-    return T.node < sv.n_nodes ? kTravState : kShadeState;
+    T.tlim = f32_up(T.closest);
+    T.pmask = 0;
+    return T.node >= 0 ? kTravState : kShadeState;
 }
 
-// Work item w (64 pixels = one 8x8 tile of the compact row space) -> pixel.
-__device__ __forceinline__ bool decode_pixel(const KernelParams& p, uint32_t item, int32_t& x, int32_t& j) {
-    const uint32_t tile = item >> 6, r = item & 63u;
+// Work item i of a band = one sample: pixel q = i / r in 8x8-tile order of the
+// band's compact rows (so a 64-item chunk is one pixel's samples at r = 64, or
+// an 8x8 tile at r = 1), sample s = i % r.
+__device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, int32_t& x, int32_t& j, uint32_t& s) {
+    const uint32_t q = i / (uint32_t)p.spp;
+    s = i - q * (uint32_t)p.spp;
+    const uint32_t tile = q >> 6, r = q & 63u;
     const uint32_t tx = tile % (uint32_t)p.tiles_x, ty = tile / (uint32_t)p.tiles_x;
     x = (int32_t)(tx * 8u + (r & 7u));
-    j = (int32_t)(ty * 8u + (r >> 3));
-    return x < p.width && j < p.rows;
+    const int32_t jb = (int32_t)(ty * 8u + (r >> 3));
+    j = p.j0 + jb;
+    return x < p.width && jb < p.band_rows;
 }
 
-// Claim pixel (x, compact row j) for the lane; its first camera ray is generated
-// by the caller (get_ray, directly or in the BVH kernel's batched phase).
-__device__ __forceinline__ void start_pixel(const KernelParams& p, Lane& L, int32_t x, int32_t j) {
+// Start sample s of pixel (x, compact row j) in the lane: its camera ray.
+__device__ __forceinline__ void start_sample(const KernelParams& p, UniPtr uni, Lane& L, uint32_t item, int32_t x,
+                                             int32_t j, uint32_t s) {
     const int32_t y = row_of(p, j);
+    L.item = item;
     L.x = x;
     L.j = j;
     L.pixel = (uint32_t)y * (uint32_t)p.width + (uint32_t)x;  // global index: tiling-independent RNG key
-    L.fx = (double)x;
-    L.fy = (double)y;
-    L.sample = 0;
+    L.sample = s;
     L.bounce = 0;
     L.segments = 0;
     L.thr = d3(1, 1, 1);
-    L.sum = d3(0, 0, 0);
     L.busy = true;
+    get_ray(p, uni, camera_block(uni, L.pixel, s), (double)x, (double)y, L.org, L.dir);
 }
 
-// A path ended with `color`: accumulate (Add(colorSum, color), ray/tracer.go:143)
-// and either set up the next sample or finish the pixel. Returns false when the
-// pixel is done (written) and the lane is free.
-template <int kFmt, bool kStats>
-__device__ __forceinline__ bool finish_sample(const KernelParams& p, Lane& L, const D3& color, Stats& st) {
-    L.sum = add(L.sum, color);
-    ++L.sample;
-    if (L.sample >= (uint32_t)p.spp) {
-        write_pixel<kFmt>(p, L);
-        if constexpr (kStats) st.segments += L.segments;
-        L.busy = false;
-        return false;
-    }
-    L.thr = d3(1, 1, 1);
-    L.bounce = 0;
-    return true;
+// A path ended with `color`: store it in the band's sample buffer (the resolve
+// kernel adds a pixel's samples in sample order, Add(colorSum, color) of
+// ray/tracer.go:143), count its segments, free the lane.
+template <bool kStats>
+__device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st) {
+    double* o = p.samples + (size_t)L.item * 3;
+    o[0] = color.x;
+    o[1] = color.y;
+    o[2] = color.z;
+    if (p.segments) atomicAdd(p.segments + (size_t)L.j * (size_t)p.width + (size_t)L.x, L.segments);
+    if constexpr (kStats) st.segments += L.segments;
+    L.busy = false;
 }
 
 // One recursion level of RayColor (ray/objects.go:49-62) after Scene.Hit gave
 // (best, closest): the sky on a miss, else the hit record and the material's
-// scatter; a path that ends is accumulated and the lane moves on to its next
-// sample's camera ray. `geo_at`/`mat_at` give the hit sphere's geometry and
-// shading record. Returns true when the lane has a new ray to trace, false when
-// its pixel is finished (written) and the lane is free.
+// scatter. `geo_at`/`mat_at` give the hit sphere's geometry and shading record.
+// Returns true when the lane has a scattered ray to trace, false when the path
+// ended (stored; the lane is free).
 //
-// Written for a wave of lanes on different branches: the work every branch
-// needs is done once, before the branches — one Philox block per lane (the
-// bounce's scatter block, or the next sample's camera block when the path ends
-// here) and the unit direction (sky, Metal, Dielectric).
-template <int kFmt, bool kStats, typename GeoAt, typename MatAt>
+// Written for a wave of lanes on different branches: the work several branches
+// need is done once, before them — the bounce's Philox block and the unit
+// direction (sky, Metal, Dielectric).
+template <bool kStats, typename GeoAt, typename MatAt>
 __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
                                            GeoAt geo_at, MatAt mat_at, Stats& st) {
     const bool hit = best >= 0;
@@ -520,8 +566,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     // (RayColor(depth 0) is black), so no scatter is computed for it.
     const bool last = L.bounce + 1u >= (uint32_t)p.max_depth;
     bool ends = !hit || last;
-    U4 u = philox_u4(uni_seed(uni), L.pixel, ends ? L.sample + 1u : L.sample, ends ? 0u : L.bounce,
-                     (ends ? kPurposeCamera : kPurposeScatter) << 24);
+    const U4 u = philox_u4(uni_seed(uni), L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
     const D3 ud = unit(L.dir);
     D3 color = d3(0, 0, 0);
     if (!hit) {  // AmbientLight.Hit (ray/objects.go:68-73)
@@ -567,17 +612,15 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         }
     }
     if (!ends) return true;
-    if (!finish_sample<kFmt, kStats>(p, L, color, st)) return false;
-    if (hit && !last) u = camera_block(uni, L.pixel, L.sample);  // absorbed: `u` was the scatter block
-    get_ray(p, uni, u, L.fx, L.fy, L.org, L.dir);
-    return true;
+    end_path<kStats>(p, L, color, st);
+    return false;
 }
 
 #ifndef TRAY_WAVES_PER_SIMD
 #define TRAY_WAVES_PER_SIMD 5
 #endif
 #ifndef TRAY_BVH_WAVES_PER_SIMD
-#define TRAY_BVH_WAVES_PER_SIMD 3
+#define TRAY_BVH_WAVES_PER_SIMD 4
 #endif
 // BVH lane scheduling: node steps per loop iteration, and how many lanes must
 // be waiting before the (expensive, FP64) leaf and shading phases run. A phase
@@ -617,8 +660,18 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 // lanes wait for them. A lane whose traversal ends early does not wait for the
 // wave's slowest ray: it shades and starts its next segment while others still
 // traverse.
-template <bool kLDS, int kFmt, bool kBVH, bool kStats>
-__global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
+// The BVH kernel runs one workgroup per CU (all its waves share one LDS copy of
+// the scene); the linear scan runs 256-lane workgroups.
+constexpr int kBvhBlock = 256 * TRAY_BVH_WAVES_PER_SIMD;
+static_assert(kBvhBlock <= 1024, "BVH workgroup larger than 1024 lanes");
+
+// LDS stack bytes of a BVH workgroup (16-bit entries, 16-byte aligned).
+__host__ __device__ constexpr size_t bvh_stack_bytes(int32_t stack_cap) {
+    return ((size_t)stack_cap * kBvhBlock * sizeof(uint16_t) + 15) / 16 * 16;
+}
+
+template <bool kLDS, bool kBVH, bool kStats>
+__global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
     extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
     __attribute__((address_space(3))) Uniforms* uni_lds =
         (__attribute__((address_space(3))) Uniforms*)reinterpret_cast<Uniforms*>(smem_all);
@@ -643,26 +696,31 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
     }
     const UniPtr uni = uni_lds;
     SceneView sv{p.geo, p.nodes, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
-    if constexpr (kLDS) {
-        if constexpr (kBVH) {
-            // [nodes: n_nodes x 32 B][bgeo: n_slots x 32 B][bidx: n_slots x 4 B]; shading
-            // records (bmat) stay in global memory (L1/L2-resident, read once per hit).
-            double4* lds_nodes = smem;
-            double4* lds_geo = smem + p.n_nodes;
-            int32_t* lds_idx = reinterpret_cast<int32_t*>(smem + p.n_nodes + p.n_slots);
+    Stack S{nullptr};
+    if constexpr (kBVH) {
+        // [stacks: stack_cap x blockDim x 2 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]
+        // [bidx: n_slots x 4 B]; shading records (bmat) stay in global memory
+        // (L1/L2-resident, read once per hit).
+        S.base = (__attribute__((address_space(3))) uint16_t*)reinterpret_cast<uint16_t*>(smem) + threadIdx.x;
+        double4* scene = smem + bvh_stack_bytes(p.stack_cap) / sizeof(double4);
+        if constexpr (kLDS) {
+            double4* lds_nodes = scene;
+            double4* lds_geo = scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4));
+            int32_t* lds_idx = reinterpret_cast<int32_t*>(lds_geo + p.n_slots);
             const double4* gn = reinterpret_cast<const double4*>(p.nodes);
-            for (int i = threadIdx.x; i < p.n_nodes; i += blockDim.x) lds_nodes[i] = gn[i];
+            const int n4 = p.n_nodes * (int)(sizeof(Bvh4Node) / sizeof(double4));
+            for (int i = threadIdx.x; i < n4; i += blockDim.x) lds_nodes[i] = gn[i];
             for (int i = threadIdx.x; i < p.n_slots; i += blockDim.x) {
                 lds_geo[i] = p.bgeo[i];
                 lds_idx[i] = p.bidx[i];
             }
-            sv.nodes = reinterpret_cast<const BvhNode*>(lds_nodes);
+            sv.nodes = reinterpret_cast<const Bvh4Node*>(lds_nodes);
             sv.bgeo = lds_geo;
             sv.bidx = lds_idx;
-        } else {
-            for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
-            sv.geo = smem;
         }
+    } else if constexpr (kLDS) {
+        for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
+        sv.geo = smem;
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -676,6 +734,7 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
     bool exhausted = false;
 #ifdef TRAY_PROFILE
     uint64_t prof[16] = {};
+    const uint64_t prof_start = __builtin_amdgcn_s_memrealtime();
 #endif
 
     while (true) {
@@ -701,9 +760,10 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                 const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
                 if (rank < take) {
                     int32_t x, j;
-                    if (decode_pixel(p, pool_next + rank, x, j)) {
-                        start_pixel(p, L, x, j);
-                        get_ray(p, uni, camera_block(uni, L.pixel, 0u), L.fx, L.fy, L.org, L.dir);
+                    uint32_t smp;
+                    const uint32_t item = pool_next + rank;
+                    if (item < p.items && decode_item(p, item, x, j, smp)) {
+                        start_sample(p, uni, L, item, x, j, smp);
                         if constexpr (kBVH) {
                             ++L.segments;
                             trav_begin(T, L.org, L.dir);
@@ -723,8 +783,8 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                 ++L.segments;
                 double closest;
                 const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
-                shade_step<kFmt, kStats>(p, uni, L, best, closest, [&] { return p.geo[best]; },
-                                         [&] { return p.mat[best]; }, st);
+                shade_step<kStats>(p, uni, L, best, closest, [&] { return p.geo[best]; },
+                                   [&] { return p.mat[best]; }, st);
             }
         } else {
             // Node steps for the traversing lanes.
@@ -737,8 +797,9 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                     PROF_CNT(4, 1);
                     PROF_CNT(5, __popcll(m));
                     if (state == kTravState) {
-                        state = trav_node(T, sv);
-                        if constexpr (kStats) ++st.boxes;
+                        uint32_t tested;
+                        state = trav_node(T, sv, S, tested);
+                        if constexpr (kStats) st.boxes += tested;
                     }
                 }
                 PROF_ADD(1);
@@ -751,8 +812,9 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                 PROF_CNT(6, 1);
                 PROF_CNT(7, __popcll(m_leaf));
                 if (state == kLeafState) {
-                    if constexpr (kStats) st.spheres += (uint64_t)(T.leaf & 7);
-                    state = trav_leaf(T, sv, L.org, L.dir);
+                    uint32_t tested;
+                    state = trav_leaf(T, sv, L.org, L.dir, tested);
+                    if constexpr (kStats) st.spheres += tested;
                 }
                 PROF_ADD(2);
             }
@@ -764,8 +826,8 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
                 PROF_CNT(8, 1);
                 PROF_CNT(9, __popcll(m_shade));
                 if (state == kShadeState) {
-                    if (shade_step<kFmt, kStats>(p, uni, L, T.best, T.closest, [&] { return sv.bgeo[T.slot]; },
-                                                 [&] { return sv.bmat[T.slot]; }, st)) {
+                    if (shade_step<kStats>(p, uni, L, T.best, T.closest, [&] { return sv.bgeo[T.slot]; },
+                                           [&] { return sv.bmat[T.slot]; }, st)) {
                         ++L.segments;
                         trav_begin(T, L.org, L.dir);
                         state = sv.n_nodes > 0 ? kTravState : kShadeState;
@@ -783,56 +845,128 @@ __global__ __launch_bounds__(256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PE
         atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
     }
 #ifdef TRAY_PROFILE
-    if (kStats && lane == 0)
-        for (int i = 0; i < 16; ++i) atomicAdd(p.stats + 3 + i, (unsigned long long)prof[i]);
+    if (kStats && lane == 0) {
+        for (int i = 0; i < 13; ++i) atomicAdd(p.stats + 3 + i, (unsigned long long)prof[i]);
+        // Wave lifetimes on the constant-rate clock: latest exit, sum of lifetimes, earliest start.
+        const uint64_t end = __builtin_amdgcn_s_memrealtime();
+        atomicMax(p.stats + 16, (unsigned long long)end);
+        atomicAdd(p.stats + 17, (unsigned long long)(end - prof_start));
+        atomicMax(p.stats + 18, (unsigned long long)~prof_start);
+        // Per-wave (start, end) from stats[32] on (the buffer must hold 32 + 2 x waves).
+        const uint32_t wave = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
+        p.stats[32 + 2 * wave] = prof_start;
+        p.stats[33 + 2 * wave] = end;
+    }
 #endif
+}
+
+// A band's pixels: the mean of each pixel's samples, added in sample order
+// (colorSum and colorSumDiv of ray/tracer.go:123-150), written in the output
+// format. One thread per pixel of the band's 8x8-tile order.
+template <int kFmt>
+__global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= p.items / (uint32_t)p.spp) return;
+    int32_t x, j;
+    uint32_t s0;
+    if (!decode_item(p, q * (uint32_t)p.spp, x, j, s0)) return;
+    const double* smp = p.samples + (size_t)q * (size_t)p.spp * 3;
+    D3 sum = d3(0, 0, 0);
+    for (int32_t s = 0; s < p.spp; ++s) sum = add(sum, d3(smp[3 * s], smp[3 * s + 1], smp[3 * s + 2]));
+    const double inv = 1.0 / (double)p.spp;  // colorSumDiv (ray/tracer.go:123)
+    const D3 mean = smul(sum, inv);
+    const size_t off = (size_t)j * (size_t)p.width + (size_t)x;
+    if constexpr (kFmt == kOutRGBF64) {
+        double* o = static_cast<double*>(p.out) + off * 3;
+        o[0] = mean.x;
+        o[1] = mean.y;
+        o[2] = mean.z;
+    } else if constexpr (kFmt == kOutRGBF32) {
+        float* o = static_cast<float*>(p.out) + off * 3;
+        o[0] = (float)mean.x;
+        o[1] = (float)mean.y;
+        o[2] = (float)mean.z;
+    } else {
+        const uint32_t rgba = linear_to_srgb(mean.x) | (linear_to_srgb(mean.y) << 8) |
+                              (linear_to_srgb(mean.z) << 16) | (255u << 24);
+        static_cast<uint32_t*>(p.out)[off] = rgba;
+    }
 }
 
 using KernelFn = void (*)(KernelParams);
 
-template <bool kLDS, bool kBVH, bool kStats>
-static KernelFn pick_fmt(int fmt) {
-    if (fmt == kOutRGBF64) return render_kernel<kLDS, kOutRGBF64, kBVH, kStats>;
-    if (fmt == kOutRGBF32) return render_kernel<kLDS, kOutRGBF32, kBVH, kStats>;
-    return render_kernel<kLDS, kOutRGBA8, kBVH, kStats>;
+static KernelFn pick_kernel(bool use_lds, bool bvh, bool stats) {
+    if (stats) {
+        if (use_lds) return bvh ? render_kernel<true, true, true> : render_kernel<true, false, true>;
+        return bvh ? render_kernel<false, true, true> : render_kernel<false, false, true>;
+    }
+    if (use_lds) return bvh ? render_kernel<true, true, false> : render_kernel<true, false, false>;
+    return bvh ? render_kernel<false, true, false> : render_kernel<false, false, false>;
 }
 
-static KernelFn pick_kernel(bool use_lds, bool bvh, bool stats, int fmt) {
-    if (stats) {  // instrumented launches (bench roofline counts) always write f32
-        if (use_lds) return bvh ? render_kernel<true, kOutRGBF32, true, true> : render_kernel<true, kOutRGBF32, false, true>;
-        return bvh ? render_kernel<false, kOutRGBF32, true, true> : render_kernel<false, kOutRGBF32, false, true>;
-    }
-    if (use_lds) return bvh ? pick_fmt<true, true, false>(fmt) : pick_fmt<true, false, false>(fmt);
-    return bvh ? pick_fmt<false, true, false>(fmt) : pick_fmt<false, false, false>(fmt);
+static KernelFn pick_resolve(int fmt) {
+    if (fmt == kOutRGBF64) return resolve_kernel<kOutRGBF64>;
+    if (fmt == kOutRGBF32) return resolve_kernel<kOutRGBF32>;
+    return resolve_kernel<kOutRGBA8>;
 }
 
 // Blocks the device keeps resident for this kernel and LDS size (persistent grid cap).
-static int resident_blocks(int device, KernelFn fn, size_t lds) {
+static int resident_blocks(int device, KernelFn fn, int threads, size_t lds) {
     hipDeviceProp_t prop;
     int cus = 256;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), 256, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), threads, lds) !=
             hipSuccess ||
         per_cu <= 0)
-        per_cu = 2;
+        per_cu = 1;
     return cus * per_cu;
+}
+
+size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t stack_cap) {
+    return kUniformsBytes + bvh_stack_bytes(stack_cap) + (size_t)n_nodes * sizeof(Bvh4Node) +
+           (size_t)n_slots * (sizeof(double4) + sizeof(int32_t));
+}
+
+// Bands of 8-row tile rows, each <= kMaxBandSamples samples (at least one tile row).
+static int32_t band_tile_rows(int32_t width, int32_t spp) {
+    const uint64_t per = (uint64_t)((width + 7) / 8) * 64u * (uint64_t)spp;
+    return (int32_t)std::max<uint64_t>(1, kMaxBandSamples / per);
+}
+
+size_t sample_buffer_bytes(int32_t width, int32_t rows, int32_t spp) {
+    if (rows <= 0) return 0;
+    const int32_t tile_rows = std::min(band_tile_rows(width, spp), (rows + 7) / 8);
+    return (size_t)((width + 7) / 8) * 64u * (size_t)tile_rows * (size_t)spp * 3 * sizeof(double);
+}
+
+bool band_fits(int32_t width, int32_t spp) {
+    return (uint64_t)((width + 7) / 8) * 64u * (uint64_t)spp <= 0x7FFFFFFFull;
 }
 
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (p.rows <= 0) return hipSuccess;
+    if (!band_fits(p.width, p.spp)) return hipErrorInvalidValue;
     p.tiles_x = (p.width + 7) / 8;
-    const uint32_t tiles_y = (uint32_t)((p.rows + 7) / 8);
-    p.nchunks = (uint32_t)p.tiles_x * tiles_y;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    const size_t lds_bytes = use_bvh ? (size_t)p.n_nodes * sizeof(BvhNode) + (size_t)p.n_slots * (sizeof(double4) + 4)
-                                     : (size_t)p.n_pad * sizeof(double4);
-    const bool use_lds = lds_bytes + kUniformsBytes <= kMaxLDSBytes;
-    const size_t lds = kUniformsBytes + (use_lds ? (lds_bytes + 15) / 16 * 16 : 0);
+    bool use_lds;
+    size_t lds;
+    if (use_bvh) {
+        const size_t full = bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.stack_cap);
+        use_lds = full <= kMaxLDSBytes;
+        lds = use_lds ? (full + 15) / 16 * 16 : kUniformsBytes + bvh_stack_bytes(p.stack_cap);
+        if (lds > kMaxLDSBytes) return hipErrorInvalidValue;  // stack bound checked when the scene is built
+    } else {
+        const size_t geo = (size_t)p.n_pad * sizeof(double4);
+        use_lds = geo + kUniformsBytes <= kMaxLDSBytes;
+        lds = kUniformsBytes + (use_lds ? geo : 0);
+    }
+    const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
-    const KernelFn fn = pick_kernel(use_lds, use_bvh, stats, p.out_format);
+    const KernelFn fn = pick_kernel(use_lds, use_bvh, stats);
+    const KernelFn resolve = pick_resolve(p.out_format);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {
         int dev;
@@ -846,20 +980,13 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     for (const Setup& c : cache)
         if (c.fn == fn && c.dev == dev && c.lds == lds && c.blocks > 0) blocks = c.blocks;
     if (blocks == 0) {
-        if (use_lds) {
-            e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kMaxLDSBytes);
-            if (e != hipSuccess) return e;
-        }
-        blocks = resident_blocks(dev, fn, lds);
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kMaxLDSBytes);
+        if (e != hipSuccess) return e;
+        blocks = resident_blocks(dev, fn, threads, lds);
         cache[cache_next] = Setup{dev, fn, lds, blocks};
         cache_next = (cache_next + 1) % 8;
     }
-    // Enough waves for every item, capped at what the device keeps resident.
-    const uint32_t want = (p.nchunks + 3u) / 4u;
-    const uint32_t grid = std::min<uint32_t>(want, (uint32_t)blocks);
-    e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
     if (stats) {
 #ifdef TRAY_PROFILE
         e = hipMemsetAsync(p.stats, 0, 19 * sizeof(unsigned long long), stream);
@@ -868,8 +995,30 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
 #endif
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, stream, p);
-    return hipGetLastError();
+    if (p.segments) {  // summed per path with atomics
+        e = hipMemsetAsync(p.segments, 0, (size_t)p.rows * (size_t)p.width * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+    }
+    const int32_t band = band_tile_rows(p.width, p.spp) * 8;
+    const uint32_t waves = (uint32_t)threads / 64u;
+    for (int32_t j0 = 0; j0 < p.rows; j0 += band) {
+        p.j0 = j0;
+        p.band_rows = std::min(band, p.rows - j0);
+        const uint32_t pixels = (uint32_t)p.tiles_x * (uint32_t)((p.band_rows + 7) / 8) * 64u;
+        p.items = pixels * (uint32_t)p.spp;
+        p.nchunks = (p.items + 63u) / 64u;
+        // Enough waves for every chunk, capped at what the device keeps resident.
+        const uint32_t grid = std::min<uint32_t>((p.nchunks + waves - 1u) / waves, (uint32_t)blocks);
+        e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(threads), lds, stream, p);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(resolve, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, p);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace tray

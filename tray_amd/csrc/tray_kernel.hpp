@@ -50,12 +50,16 @@ struct KernelParams {
     int32_t n;
     int32_t n_pad;       // round_up(n, 4) + 4
     int32_t tiles_x;     // 8x8 pixel tiles per compact row band
-    uint32_t nchunks;    // 64-pixel work items
-    const BvhNode* nodes;   // exact-culling BVH (tray_bvh.cpp), depth-first
-    const double4* bgeo;    // spheres in leaf-slot order, + kBvhLeafMax NaN slots
+    uint32_t nchunks;    // 64-item chunks of the band's work items (one item = one sample)
+    uint32_t items;      // band work items: 8x8-tile-padded pixels x spp
+    int32_t j0, band_rows;  // the band: compact rows [j0, j0 + band_rows)
+    double* samples;     // per-item path colours (3 doubles), summed in order by the resolve kernel
+    const Bvh4Node* nodes;  // exact-culling 4-wide BVH (tray_bvh.cpp), root first
+    const double4* bgeo;    // spheres in leaf-slot order
     const int32_t* bidx;    // original index per slot
     const MatRec* bmat;     // shading record per slot
     int32_t n_nodes, n_slots;
+    int32_t stack_cap;      // traversal stack slots per lane (Bvh::stack_max + 1)
     unsigned long long* stats;  // nullable: [segments, sphere tests, box tests]
     int32_t width, height, spp, max_depth;
     int32_t y_start, rows, tile_rows, tile_count, tile_index;
@@ -70,6 +74,17 @@ struct KernelParams {
 };
 
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
+
+// Samples per launch band (the sample buffer holds one band: 24 B per sample).
+constexpr uint64_t kMaxBandSamples = 1ull << 26;
+// Bytes of sample buffer launch_render needs for `rows` compact rows.
+size_t sample_buffer_bytes(int32_t width, int32_t rows, int32_t spp);
+// False when one 8-row band has more than 2^31 samples (item indices are 32-bit).
+bool band_fits(int32_t width, int32_t spp);
+
+// LDS the BVH kernel needs to hold the whole BVH scene (plus its traversal
+// stacks) on chip; above kMaxLDSBytes it reads the scene from global memory.
+size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t stack_cap);
 
 // Padded geometry length for n spheres (see KernelParams::geo).
 inline int32_t padded_spheres(int32_t n) { return ((n + 3) / 4) * 4 + 4; }
