@@ -13,14 +13,19 @@ frame is fixed as N grows). value = W*H*r*steps / max-over-ranks wall time.
 
 Also reported (rank 0):
   roofline     the megakernel against the VALU roof (it is compute bound; HBM
-               traffic is ~1e-5 of the roof and reported under "hbm"):
-               achieved = algorithmic VALU work per launch / mean kernel time,
-               in FP64-instruction equivalents: FP64 ops = 17 per ray-sphere
-               test + 60 per segment + 40 per sample; FP32
-               ops = 19 per ray-box test of the exact-culling BVH, counted at
-               half weight (FP32 issues at 2x the FP64 rate). Tests, segments
-               and box tests are counted by the kernel itself in an untimed
-               instrumented launch (segments are bit-exact with the oracle).
+               traffic is far below its roof and reported under "hbm"):
+               achieved = algorithmic VALU work per launch / mean launch time,
+               in lane-ops (every non-packed FP32/FP64 VALU op takes the same
+               issue slot; no FMA is allowed in the FP64 arithmetic, so the peak
+               is 78.6 TFLOP/s / 2 = 39.3 T ops/s). Work = 17 FP64 ops per
+               ray-sphere test + 60 per segment + 40 per sample
+               + 11 FP32 ops per ray-box test of the exact-culling BVH (6 FMA + 5
+               min/max/compare). Segments, sphere and box tests are counted by the
+               kernel itself in an untimed instrumented launch (segments are
+               bit-exact with the oracle). The timed launch is the megakernel plus
+               its per-pixel resolve pass (both kernels are on the stream between
+               the two HIP events); "brute_force_equiv" rates the same frame at the
+               reference's all-spheres-per-segment work.
   cpu_baseline the oracle (C port of the reference's CPU loop with the
                reference's chunk-queue scheduler, ray/tracer.go:86-116) timed on
                a bounded row sample of the same frame on the host cores.
@@ -61,7 +66,7 @@ def main() -> int:
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--tile-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-row-step", type=int, default=12, help="oracle renders every k-th row of the frame")
+    ap.add_argument("--cpu-row-step", type=int, default=2, help="oracle renders every k-th row of the frame")
     ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")
     args = ap.parse_args()
 
@@ -159,10 +164,13 @@ def main() -> int:
     if rank == 0:
         local_samples = rows * W * spp
         ops64 = 17.0 * sphere_tests + 60.0 * segments_local + 40.0 * local_samples
-        ops32 = 19.0 * box_tests
-        ops = ops64 + 0.5 * ops32
+        ops32 = 11.0 * box_tests
+        ops = ops64 + ops32
+        brute = 17.0 * len(spheres) * segments_local + 60.0 * segments_local + 40.0 * local_samples
         achieved = ops / (kernel_ms * 1e-3) / 1e12
-        out_bytes = rows * W * 12 + len(spheres) * (32 + 48)
+        # megakernel: one 24-B colour per sample into the sample buffer + the scene
+        # (the resolve pass then reads the buffer and writes the float3 image)
+        out_bytes = local_samples * 24 + len(spheres) * (32 + 64)
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
         if os.path.exists(pmc_path):
@@ -183,11 +191,15 @@ def main() -> int:
             "box_tests_per_launch": box_tests,
             "fp64_ops_per_launch": ops64,
             "fp32_ops_per_launch": ops32,
-            "ops_model": "FP64-instruction equivalents: 17/sphere test + 60/segment + 40/sample (FP64, no FMA; "
-                         "SURVEY.md 8d) + 0.5 x 19/box test (FP32); peak = 78.6 TFLOP/s FP64 vector spec / 2",
-            "traversal": "linear scan" if args.linear else "exact-culling BVH",
+            "ops_model": "VALU lane-ops: 17/sphere test + 60/segment + 40/sample (FP64, no FMA; SURVEY.md 8d) "
+                         "+ 11/box test (FP32); peak = 78.6 TFLOP/s FP64 vector spec / 2 = 39.3 T ops/s",
+            "brute_force_equiv": {"ops_per_launch": brute,
+                                  "TFLOPs": round(brute / (kernel_ms * 1e-3) / 1e12, 3),
+                                  "note": "reference work (every sphere tested per segment) / measured time"},
+            "traversal": "linear scan" if args.linear else "exact-culling 4-wide BVH",
             "hbm": {"achieved_GBs": round(out_bytes / (kernel_ms * 1e-3) / 1e9, 3), "peak_GBs": HBM_PEAK_GBS,
-                    "algorithmic_bytes_per_launch": out_bytes, "note": "not the bound"},
+                    "algorithmic_bytes_per_launch": out_bytes,
+                    "note": "not the bound; megakernel only (traffic: profiles/pmc_<config>.json)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed,

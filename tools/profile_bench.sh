@@ -1,0 +1,15 @@
+#!/bin/bash
+# Kernel-trace stats and HBM counters of the default bench command (run on the
+# GPU box from the repo root). Each rocprofv3 pass is its own run; --pmc passes
+# never combine tracing domains.
+#   usage: tools/profile_bench.sh <outdir> [bench.py args...]
+set -u
+OUT=${1:-gpurun_out/prof}; shift || true
+ARGS=${*:-"--steps 5 --warmup 1 --no-cpu-baseline"}
+export TMPDIR=/tmp
+mkdir -p "$OUT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py $ARGS > "$OUT/kt.log" 2>&1 || exit 1
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex render_kernel -d "$OUT/$C" -o pmc --output-format csv -- python3 bench.py $ARGS > "$OUT/$C.log" 2>&1 || exit 1
+done
+echo done > "$OUT/status.txt"
