@@ -17,29 +17,31 @@ constexpr int kBvhWidth = 4;
 constexpr int kBvhLeafMax = 4;
 // Below this many spheres the linear scan is used (no BVH is built).
 constexpr int kBvhMinSpheres = 16;
-// child[] value of an unused child slot.
-constexpr int32_t kBvhEmpty = 0x7fffffff;
-// Traversal stack entries are 16-bit node indices.
-constexpr int32_t kBvhMaxNodes = 65535;
+// Child references are 16 bits: an inner node index (< 0x8000), 0x8000 | leaf
+// index, or kBvhNone for an unused child slot (whose box is empty).
+constexpr uint32_t kBvhLeafBit = 0x8000u;
+constexpr uint32_t kBvhNone = 0xFFFFu;
+constexpr int32_t kBvhMaxNodes = 0x8000;
+constexpr int32_t kBvhMaxLeaves = 0x7FFF;
 
 // 128 B: the boxes of up to four children, SoA by axis so one node is seven
 // 16-byte LDS reads; box[a][0] / box[a][1] are the low / high planes on axis a
-// (16 B apart, so a lane picks its near and far planes by address).
-// child[k] >= 0: inner node index; child[k] < 0: leaf ~((first slot << 3) |
-// count); kBvhEmpty: unused (its box is empty: lo = +inf, hi = -inf).
+// (16 B apart, so a lane picks its near and far planes by address). An unused
+// child's box is empty (lo = +inf, hi = -inf) and its ref is kBvhNone.
 struct Bvh4Node {
     float box[3][2][kBvhWidth];  // [axis][lo, hi][child]
-    int32_t child[kBvhWidth];
-    int32_t pad[4];
+    uint32_t ref[kBvhWidth];     // 16-bit child references (above)
+    uint32_t pad[4];
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
 
 struct Bvh {
     std::vector<Bvh4Node> nodes;  // nodes[0] is the root (always an inner node)
+    std::vector<int32_t> leaves;  // per leaf: (first slot << 3) | sphere count
     std::vector<double4> geo;     // {cx, cy, cz, R*R} in leaf-slot order
     std::vector<int32_t> idx;     // original list index of each slot
     double bound = 0;             // M: every box coordinate lies in [-M, M]
-    int32_t stack_max = 0;        // deepest stack the near-first traversal can build
+    int32_t stack_max = 0;        // deepest stack the ordered traversal can build
     int leaf_max = 1;
 };
 

@@ -102,8 +102,9 @@ struct tray_scene_s {
     // exact-culling BVH (absent for tiny or non-finite scenes)
     bool has_bvh;
     double bvh_bound;
-    int32_t n_nodes, n_slots, stack_cap;
+    int32_t n_nodes, n_slots, n_leaves, stack_cap;
     tray::Bvh4Node* nodes;
+    int32_t* leaves;
     double4* bgeo;
     int32_t* bidx;
     tray::MatRec* bmat;
@@ -222,8 +223,9 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
             Bvh b;
             if (!build_bvh(spheres, n, &b, leaf_max)) continue;
             const int32_t cap = b.stack_max + 1;  // + the scratch slot (tray_kernel.hip Stack)
-            if (bvh_scene_lds_bytes(0, 0, cap) > kMaxLDSBytes) continue;  // stack alone too deep
-            const bool fits = bvh_scene_lds_bytes((int32_t)b.nodes.size(), (int32_t)b.geo.size(), cap) <= kMaxLDSBytes;
+            if (bvh_scene_lds_bytes(0, 0, 0, cap) > kMaxLDSBytes) continue;  // stack alone too deep
+            const bool fits = bvh_scene_lds_bytes((int32_t)b.nodes.size(), (int32_t)b.geo.size(),
+                                                  (int32_t)b.leaves.size(), cap) <= kMaxLDSBytes;
             if (!has_bvh || fits) {
                 bvh = std::move(b);
                 has_bvh = true;
@@ -237,6 +239,8 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->bvh_bound = bvh.bound;
     sc->n_nodes = (int32_t)bvh.nodes.size();
     sc->n_slots = (int32_t)bvh.geo.size();
+    sc->n_leaves = (int32_t)bvh.leaves.size();
+    sc->leaves = nullptr;
     sc->stack_cap = bvh.stack_max + 1;
     sc->nodes = nullptr;
     sc->bgeo = nullptr;
@@ -264,6 +268,9 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess && has_bvh) {
         e = hipMalloc(&sc->nodes, sizeof(Bvh4Node) * bvh.nodes.size());
+        if (e == hipSuccess) e = hipMalloc(&sc->leaves, sizeof(int32_t) * bvh.leaves.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->leaves, bvh.leaves.data(), sizeof(int32_t) * bvh.leaves.size(), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&sc->bgeo, sizeof(double4) * bvh.geo.size());
         if (e == hipSuccess) e = hipMalloc(&sc->bidx, sizeof(int32_t) * bvh.idx.size());
         if (e == hipSuccess)
@@ -281,6 +288,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         (void)hipFree(sc->mat);
         (void)hipFree(sc->queue);
         (void)hipFree(sc->nodes);
+        (void)hipFree(sc->leaves);
         (void)hipFree(sc->bgeo);
         (void)hipFree(sc->bidx);
         (void)hipFree(sc->bmat);
@@ -298,6 +306,7 @@ int tray_scene_release(tray_scene_t sc) {
     if (sc->mat) (void)hipFree(sc->mat);
     if (sc->queue) (void)hipFree(sc->queue);
     if (sc->nodes) (void)hipFree(sc->nodes);
+    if (sc->leaves) (void)hipFree(sc->leaves);
     if (sc->bgeo) (void)hipFree(sc->bgeo);
     if (sc->bidx) (void)hipFree(sc->bidx);
     if (sc->bmat) (void)hipFree(sc->bmat);
@@ -349,6 +358,8 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.bmat = sc->bmat;
     k.n_nodes = sc->n_nodes;
     k.n_slots = sc->n_slots;
+    k.n_leaves = sc->n_leaves;
+    k.leaves = sc->leaves;
     k.stack_cap = sc->stack_cap;
     // The BVH's conservative FP32 box test assumes every ray origin lies within
     // [-M, M]^3 (tray_bvh.cpp): hit points do; check the camera and lens disc.

@@ -71,6 +71,7 @@ struct Builder {
     std::vector<Prim> prims;
     std::vector<Node2> bin;
     std::vector<Bvh4Node> nodes;
+    std::vector<int32_t> leaves;
     std::vector<double4> geo;
     std::vector<int32_t> idx;
     double pad = 0;
@@ -203,9 +204,8 @@ struct Builder {
         }
         const int me = (int)nodes.size();
         nodes.push_back(Bvh4Node{});
-        int inner = 0;
-        for (int k = 0; k < cnt; ++k) inner += bin[ch[k]].count == 0;
-        const int32_t here = depth_stack + std::max(inner - 1, 0);
+        // The traversal visits the nearest hit child and pushes the others.
+        const int32_t here = depth_stack + (cnt - 1);
         stack_max = std::max(stack_max, here);
         for (int k = 0; k < kBvhWidth; ++k) {
             if (k >= cnt) {
@@ -213,7 +213,7 @@ struct Builder {
                     nodes[me].box[a][0][k] = INFINITY;
                     nodes[me].box[a][1][k] = -INFINITY;
                 }
-                nodes[me].child[k] = kBvhEmpty;
+                nodes[me].ref[k] = kBvhNone;
                 continue;
             }
             const Node2& c = bin[ch[k]];
@@ -228,10 +228,11 @@ struct Builder {
                     geo.push_back(make_double4(sp.center[0], sp.center[1], sp.center[2], sp.radius * sp.radius));
                     idx.push_back(prims[i].index);
                 }
-                nodes[me].child[k] = ~((slot << 3) | c.count);
+                nodes[me].ref[k] = kBvhLeafBit | (uint32_t)leaves.size();
+                leaves.push_back((slot << 3) | c.count);
             } else {
                 const int sub = collapse(ch[k], here, s);
-                nodes[me].child[k] = sub;
+                nodes[me].ref[k] = (uint32_t)sub;
             }
         }
         return me;
@@ -242,6 +243,7 @@ struct Builder {
 
 bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     out->nodes.clear();
+    out->leaves.clear();
     out->geo.clear();
     out->idx.clear();
     out->bound = 0;
@@ -269,8 +271,9 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     B.bin.reserve((size_t)2 * n);
     const int root = B.build2(0, n, 0);
     B.collapse(root, 0, s);
-    if ((int64_t)B.nodes.size() > kBvhMaxNodes) return false;
+    if ((int64_t)B.nodes.size() > kBvhMaxNodes || (int64_t)B.leaves.size() > kBvhMaxLeaves) return false;
     out->nodes.swap(B.nodes);
+    out->leaves.swap(B.leaves);
     out->geo.swap(B.geo);
     out->idx.swap(B.idx);
     out->bound = m;

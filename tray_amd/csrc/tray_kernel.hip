@@ -276,6 +276,7 @@ struct Stats {
 struct SceneView {
     const double4* geo;     // linear scan: list order, NaN-padded
     const Bvh4Node* nodes;  // BVH: 4-wide nodes, root first
+    const int32_t* leaves;  // BVH: per leaf (first slot << 3) | count
     const double4* bgeo;    // BVH: spheres in leaf-slot order
     const int32_t* bidx;    // BVH: original list index of each slot
     const MatRec* bmat;     // BVH: shading record of each slot
@@ -330,22 +331,38 @@ struct Trav {
     float ix, iy, iz, oix, oiy, oiz;  // FP32 ray: t = box * inv - org * inv
     float tlim;                       // closest rounded up to float
     int32_t near_x, near_y, near_z;   // byte offsets of the near planes in a node
-    int32_t node;                     // inner node to visit next, -1: none
-    int32_t pend;                     // node whose hit leaf children wait for the leaf phase
-    uint32_t pmask;                   // ... and which of its children they are
-    int32_t sp, top;                  // stack depth; its top entry (the rest is in LDS)
+    uint32_t cur;                     // child reference to visit next (kBvhNone: done)
+    uint32_t top;                     // stack top: sort key (entry distance | reference)
+    int32_t sp;                       // stack depth (the top included)
     double a, a_inv, closest;
     int32_t best;  // original list index of the closest hit (tie-break key)
     int32_t slot;  // its leaf slot (geometry + shading record)
 };
 
-// Per-lane traversal stack: 16-bit node indices in LDS, slot i of the lane at
-// base[i * blockDim.x] (consecutive lanes, consecutive banks). The top entry
+#ifndef TRAY_BVH_WAVES_PER_SIMD
+#define TRAY_BVH_WAVES_PER_SIMD 4
+#endif
+// The BVH kernel runs one workgroup per CU (all its waves share one LDS copy of
+// the scene); the linear scan runs 256-lane workgroups.
+constexpr int kBvhBlock = 256 * TRAY_BVH_WAVES_PER_SIMD;
+static_assert(kBvhBlock <= 1024, "BVH workgroup larger than 1024 lanes");
+
+// Per-lane traversal stack of sort keys in LDS, slot i of the lane at
+// base[i * kBvhBlock] (consecutive lanes, consecutive banks). The top entry
 // lives in Trav::top and slot i >= 1 holds the entry below the i-th; slot 0 is
-// a scratch slot, so pushes and pops need no branches (stack_cap = depth + 1).
+// a scratch slot, so pushes need no branches (stack_cap = depth + 1).
 struct Stack {
-    __attribute__((address_space(3))) uint16_t* base;  // this lane's slot 0
+    __attribute__((address_space(3))) uint32_t* base;  // this lane's slot 0
 };
+
+// Sort key of a hit child: the upper 16 bits of its entry distance (tn >= 0, so
+// keys order like distances, to bf16 precision, and never exceed the true tn)
+// over its 16-bit reference. ~0 = no entry.
+__device__ __forceinline__ float key_tn(uint32_t key) { return __uint_as_float(key & 0xFFFF0000u); }
+
+__device__ __forceinline__ uint32_t state_of(uint32_t ref) {
+    return ref == kBvhNone ? kShadeState : (ref & kBvhLeafBit) ? kLeafState : kTravState;
+}
 
 __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir) {
     T.a = length_sq(dir);  // hoisted: same bits as per sphere
@@ -354,10 +371,9 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
     T.best = -1;
     T.slot = 0;
     T.tlim = __builtin_inff();
-    T.node = 0;
-    T.pmask = 0;
+    T.cur = 0;  // the root
     T.sp = 0;
-    T.top = 0;
+    T.top = ~0u;
     float dxf = (float)dir.x, dyf = (float)dir.y, dzf = (float)dir.z;
     if (__builtin_fabsf(dxf) < 1e-30f) dxf = 1e-30f;
     if (__builtin_fabsf(dyf) < 1e-30f) dyf = 1e-30f;
@@ -375,13 +391,27 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
     T.near_z = T.iz < 0.0f ? 80 : 64;
 }
 
-// Push the node in sort key `key` if the key is valid. The store is
-// unconditional: with no push it writes slot sp, above the stack.
+// Push `key` if valid. The store is unconditional: with no push it writes
+// slot sp, above the stack.
 __device__ __forceinline__ void stack_push(Trav& T, const Stack& S, uint32_t key) {
     const bool valid = key != ~0u;
-    S.base[T.sp * (int32_t)blockDim.x] = (uint16_t)T.top;
-    T.top = valid ? (int32_t)(key & 0xFFFFu) : T.top;
+    S.base[T.sp * kBvhBlock] = T.top;
+    T.top = valid ? key : T.top;
     T.sp += valid ? 1 : 0;
+}
+
+// Pop entries until one whose box may still hold a closer hit (key_tn <= tlim:
+// the test of the box against the current closest hit, as at push time); its
+// reference, or kBvhNone. `below` = slot sp - 1, read ahead.
+__device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stack& S, uint32_t below) {
+    while (T.sp > 0) {
+        const uint32_t key = T.top;
+        --T.sp;
+        T.top = below;
+        if (key_tn(key) <= T.tlim) return key & 0xFFFFu;
+        if (T.sp > 0) below = S.base[(T.sp - 1) * kBvhBlock];
+    }
+    return kBvhNone;
 }
 
 // 1: slab distances of two children per packed FMA (v_pk_fma_f32).
@@ -389,11 +419,11 @@ __device__ __forceinline__ void stack_push(Trav& T, const Stack& S, uint32_t key
 #define TRAY_PK_FMA 0
 #endif
 
-// One node visit: test the four child boxes; hit leaf children are handed to
-// the leaf phase, the nearest hit inner child is visited next and the other hit
-// inner children are pushed far-to-near. Returns the new lane state.
+// One node visit: test the four child boxes, visit the nearest hit child next
+// (an inner node or a leaf) and push the other hit children far-to-near.
+// Returns the new lane state.
 __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, const Stack& S, uint32_t& tested) {
-    const char* nb = reinterpret_cast<const char*>(sv.nodes + T.node);
+    const char* nb = reinterpret_cast<const char*>(sv.nodes + T.cur);
     // Near and far planes of the four children on each axis (far = near ^ 16).
     const float4 nx = *reinterpret_cast<const float4*>(nb + T.near_x);
     const float4 fx = *reinterpret_cast<const float4*>(nb + (T.near_x ^ 16));
@@ -401,32 +431,29 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
     const float4 fy = *reinterpret_cast<const float4*>(nb + (T.near_y ^ 16));
     const float4 nz = *reinterpret_cast<const float4*>(nb + T.near_z);
     const float4 fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ 16));
-    const int4 ch = *reinterpret_cast<const int4*>(nb + 96);
-    // Entry below the top, read ahead for a pop (slot max(sp - 1, 0)).
-    const int32_t below = (int32_t)S.base[max(T.sp - 1, 0) * (int32_t)blockDim.x];
-    const int32_t child[4] = {ch.x, ch.y, ch.z, ch.w};
+    const uint4 rf = *reinterpret_cast<const uint4*>(nb + 96);
+    const uint32_t below = S.base[max(T.sp - 1, 0) * kBvhBlock];  // read ahead for a pop
+    const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
 #if TRAY_PK_FMA
     typedef float tray_f2 __attribute__((ext_vector_type(2)));
-    // Slab distances, two children per packed FMA: t = plane * inv - org * inv.
     const tray_f2 ixv = {T.ix, T.ix}, iyv = {T.iy, T.iy}, izv = {T.iz, T.iz};
     const tray_f2 oxv = {-T.oix, -T.oix}, oyv = {-T.oiy, -T.oiy}, ozv = {-T.oiz, -T.oiz};
-    const tray_f2 tnx01 = __builtin_elementwise_fma(tray_f2{nx.x, nx.y}, ixv, oxv), tnx23 = __builtin_elementwise_fma(tray_f2{nx.z, nx.w}, ixv, oxv);
-    const tray_f2 tfx01 = __builtin_elementwise_fma(tray_f2{fx.x, fx.y}, ixv, oxv), tfx23 = __builtin_elementwise_fma(tray_f2{fx.z, fx.w}, ixv, oxv);
-    const tray_f2 tny01 = __builtin_elementwise_fma(tray_f2{ny.x, ny.y}, iyv, oyv), tny23 = __builtin_elementwise_fma(tray_f2{ny.z, ny.w}, iyv, oyv);
-    const tray_f2 tfy01 = __builtin_elementwise_fma(tray_f2{fy.x, fy.y}, iyv, oyv), tfy23 = __builtin_elementwise_fma(tray_f2{fy.z, fy.w}, iyv, oyv);
-    const tray_f2 tnz01 = __builtin_elementwise_fma(tray_f2{nz.x, nz.y}, izv, ozv), tnz23 = __builtin_elementwise_fma(tray_f2{nz.z, nz.w}, izv, ozv);
-    const tray_f2 tfz01 = __builtin_elementwise_fma(tray_f2{fz.x, fz.y}, izv, ozv), tfz23 = __builtin_elementwise_fma(tray_f2{fz.z, fz.w}, izv, ozv);
+#define TRAY_PK(v, iv, ov, lo, hi) \
+    const tray_f2 lo = __builtin_elementwise_fma(tray_f2{v.x, v.y}, iv, ov), hi = __builtin_elementwise_fma(tray_f2{v.z, v.w}, iv, ov);
+    TRAY_PK(nx, ixv, oxv, tnx01, tnx23) TRAY_PK(fx, ixv, oxv, tfx01, tfx23)
+    TRAY_PK(ny, iyv, oyv, tny01, tny23) TRAY_PK(fy, iyv, oyv, tfy01, tfy23)
+    TRAY_PK(nz, izv, ozv, tnz01, tnz23) TRAY_PK(fz, izv, ozv, tfz01, tfz23)
+#undef TRAY_PK
     const float tnx[4] = {tnx01.x, tnx01.y, tnx23.x, tnx23.y}, tfx[4] = {tfx01.x, tfx01.y, tfx23.x, tfx23.y};
     const float tny[4] = {tny01.x, tny01.y, tny23.x, tny23.y}, tfy[4] = {tfy01.x, tfy01.y, tfy23.x, tfy23.y};
     const float tnz[4] = {tnz01.x, tnz01.y, tnz23.x, tnz23.y}, tfz[4] = {tfz01.x, tfz01.y, tfz23.x, tfz23.y};
 #else
-    // Slab distances: t = plane * inv - org * inv.
     const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
     const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
     const float nza[4] = {nz.x, nz.y, nz.z, nz.w}, fza[4] = {fz.x, fz.y, fz.z, fz.w};
     float tnx[4], tfx[4], tny[4], tfy[4], tnz[4], tfz[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 4; ++k) {  // slab distances: t = plane * inv - org * inv
         tnx[k] = __builtin_fmaf(nxa[k], T.ix, -T.oix);
         tfx[k] = __builtin_fmaf(fxa[k], T.ix, -T.oix);
         tny[k] = __builtin_fmaf(nya[k], T.iy, -T.oiy);
@@ -435,23 +462,16 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
         tfz[k] = __builtin_fmaf(fza[k], T.iz, -T.oiz);
     }
 #endif
-    // Hit inner children: upper 16 bits of the entry distance | node index (tn >= 0,
-    // so the keys order like the distances, to bf16 precision); anything else ~0.
-    // An empty child's planes are (+inf, -inf): tn = +inf, never a hit.
+    // An unused child's planes are (+inf, -inf): tn = +inf, never a hit.
     uint32_t key[4];
-    uint32_t leaves = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx[k], tny[k]), tnz[k]), 0.0f);
         const float tf = __builtin_fminf(__builtin_fminf(__builtin_fminf(tfx[k], tfy[k]), tfz[k]), T.tlim);
-        const uint32_t hit = (uint32_t)(tn <= tf);
-        const uint32_t inner = (uint32_t)(child[k] >= 0);
-        const uint32_t keep = 0u - (hit & inner);  // all ones iff a hit inner child
-        key[k] = (((__float_as_uint(tn) & 0xFFFF0000u) | (uint32_t)child[k]) & keep) | ~keep;
-        leaves |= (hit & (inner ^ 1u)) << k;
+        key[k] = tn <= tf ? ((__float_as_uint(tn) & 0xFFFF0000u) | ref[k]) : ~0u;
     }
-    tested = (uint32_t)(child[0] != kBvhEmpty) + (uint32_t)(child[1] != kBvhEmpty) +
-             (uint32_t)(child[2] != kBvhEmpty) + (uint32_t)(child[3] != kBvhEmpty);
+    tested = (uint32_t)(ref[0] != kBvhNone) + (uint32_t)(ref[1] != kBvhNone) + (uint32_t)(ref[2] != kBvhNone) +
+             (uint32_t)(ref[3] != kBvhNone);
 #define TRAY_CX(i, j)                             \
     {                                             \
         const uint32_t lo_ = min(key[i], key[j]); \
@@ -460,59 +480,63 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
     }
     TRAY_CX(0, 1) TRAY_CX(2, 3) TRAY_CX(0, 2) TRAY_CX(1, 3) TRAY_CX(1, 2)
 #undef TRAY_CX
-    stack_push(T, S, key[3]);
-    stack_push(T, S, key[2]);
-    stack_push(T, S, key[1]);
-    const int32_t here = T.node;
-    const bool has = key[0] != ~0u;
-    const bool pop = !has && T.sp > 0;
-    T.node = has ? (int32_t)(key[0] & 0xFFFFu) : pop ? T.top : -1;
-    T.top = pop ? below : T.top;
-    T.sp -= pop ? 1 : 0;
-    if (leaves != 0u) {
-        T.pend = here;
-        T.pmask = leaves;
-        return kLeafState;
+    if (key[0] != ~0u) {
+        stack_push(T, S, key[3]);
+        stack_push(T, S, key[2]);
+        stack_push(T, S, key[1]);
+        T.cur = key[0] & 0xFFFFu;
+    } else {
+        T.cur = stack_pop(T, S, below);
     }
-    return T.node >= 0 ? kTravState : kShadeState;
+    return state_of(T.cur);
 }
 
-// Test the pending leaf children's spheres (FP64, any-order rule). Each lane
-// walks its own leaves, so the wave pays for max-over-lanes(spheres) tests.
-__device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const D3& org, const D3& dir,
-                                              uint32_t& tested) {
-    const int4 ch = reinterpret_cast<const int4*>(sv.nodes + T.pend)[6];
-    uint32_t m = T.pmask;
+// Test the spheres of leaf T.cur (FP64, any-order rule), then pop the next entry.
+__device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const Stack& S, const D3& org,
+                                              const D3& dir, uint32_t& tested) {
+    const uint32_t below = S.base[max(T.sp - 1, 0) * kBvhBlock];  // read ahead for the pop
+    const int32_t info = sv.leaves[T.cur & (kBvhLeafBit - 1u)];
+    const int32_t first = info >> 3, end = first + (info & 7);
     tested = 0;
-    while (m != 0u) {
-        const uint32_t k = (uint32_t)__builtin_ctz(m);
-        m &= m - 1u;
-        const int32_t ref = ~(k == 0u ? ch.x : k == 1u ? ch.y : k == 2u ? ch.z : ch.w);
-        const int32_t first = ref >> 3, end = first + (ref & 7);
-        for (int32_t slot = first; slot < end; ++slot) {
-            double h, d;
-            quad(sv.bgeo[slot], org, dir, T.a, h, d);
-            if (d >= 0) {
-                const int32_t before = T.best;
-                candidate_any_order(h, d, T.a, T.a_inv, sv.bidx[slot], T.closest, T.best);
-                if (T.best != before) T.slot = slot;
-            }
-            ++tested;
+    for (int32_t slot = first; slot < end; ++slot) {
+        double h, d;
+        quad(sv.bgeo[slot], org, dir, T.a, h, d);
+        if (d >= 0) {
+            const int32_t before = T.best;
+            candidate_any_order(h, d, T.a, T.a_inv, sv.bidx[slot], T.closest, T.best);
+            if (T.best != before) T.slot = slot;
         }
+        ++tested;
     }
     T.tlim = f32_up(T.closest);
-    T.pmask = 0;
-    return T.node >= 0 ? kTravState : kShadeState;
+    T.cur = stack_pop(T, S, below);
+    return state_of(T.cur);
 }
 
 // Work item i of a band = one sample: pixel q = i / r in 8x8-tile order of the
 // band's compact rows (so a 64-item chunk is one pixel's samples at r = 64, or
 // an 8x8 tile at r = 1), sample s = i % r.
+// n / d for n < 2^32 through the FP64 reciprocal (rinv = RN(1/d)): the product
+// is within 2^-20 of n/d, so its floor is off by at most one; one correction step.
+__device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t d, double rinv, uint32_t& rem) {
+    int64_t q = (int64_t)((double)n * rinv);
+    int64_t r = (int64_t)n - q * (int64_t)d;
+    if (r < 0) {
+        --q;
+        r += d;
+    } else if (r >= (int64_t)d) {
+        ++q;
+        r -= d;
+    }
+    rem = (uint32_t)r;
+    return (uint32_t)q;
+}
+
 __device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, int32_t& x, int32_t& j, uint32_t& s) {
-    const uint32_t q = i / (uint32_t)p.spp;
-    s = i - q * (uint32_t)p.spp;
+    const uint32_t q = udiv(i, (uint32_t)p.spp, p.inv_spp, s);
     const uint32_t tile = q >> 6, r = q & 63u;
-    const uint32_t tx = tile % (uint32_t)p.tiles_x, ty = tile / (uint32_t)p.tiles_x;
+    uint32_t tx;
+    const uint32_t ty = udiv(tile, (uint32_t)p.tiles_x, p.inv_tiles_x, tx);
     x = (int32_t)(tx * 8u + (r & 7u));
     const int32_t jb = (int32_t)(ty * 8u + (r >> 3));
     j = p.j0 + jb;
@@ -619,20 +643,21 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #ifndef TRAY_WAVES_PER_SIMD
 #define TRAY_WAVES_PER_SIMD 5
 #endif
-#ifndef TRAY_BVH_WAVES_PER_SIMD
-#define TRAY_BVH_WAVES_PER_SIMD 4
-#endif
 // BVH lane scheduling: node steps per loop iteration, and how many lanes must
 // be waiting before the (expensive, FP64) leaf and shading phases run. A phase
 // also runs whenever nothing else can make progress.
 #ifndef TRAY_NODE_STEPS
-#define TRAY_NODE_STEPS 2
+#define TRAY_NODE_STEPS 1
 #endif
 #ifndef TRAY_LEAF_BATCH
 #define TRAY_LEAF_BATCH 24
 #endif
 #ifndef TRAY_SHADE_BATCH
-#define TRAY_SHADE_BATCH 32
+#define TRAY_SHADE_BATCH 40
+#endif
+// Idle lanes are refilled (a camera ray each) once this many wait, or the whole wave does.
+#ifndef TRAY_REFILL_BATCH
+#define TRAY_REFILL_BATCH 16
 #endif
 
 // Diagnostic build only (-DTRAY_PROFILE): per-wave s_memtime stamps around each
@@ -660,14 +685,10 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 // lanes wait for them. A lane whose traversal ends early does not wait for the
 // wave's slowest ray: it shades and starts its next segment while others still
 // traverse.
-// The BVH kernel runs one workgroup per CU (all its waves share one LDS copy of
-// the scene); the linear scan runs 256-lane workgroups.
-constexpr int kBvhBlock = 256 * TRAY_BVH_WAVES_PER_SIMD;
-static_assert(kBvhBlock <= 1024, "BVH workgroup larger than 1024 lanes");
 
-// LDS stack bytes of a BVH workgroup (16-bit entries, 16-byte aligned).
+// LDS stack bytes of a BVH workgroup (32-bit entries).
 __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t stack_cap) {
-    return ((size_t)stack_cap * kBvhBlock * sizeof(uint16_t) + 15) / 16 * 16;
+    return (size_t)stack_cap * kBvhBlock * sizeof(uint32_t);
 }
 
 template <bool kLDS, bool kBVH, bool kStats>
@@ -695,18 +716,19 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         u->seed = p.seed;
     }
     const UniPtr uni = uni_lds;
-    SceneView sv{p.geo, p.nodes, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
+    SceneView sv{p.geo, p.nodes, p.leaves, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
     Stack S{nullptr};
     if constexpr (kBVH) {
-        // [stacks: stack_cap x blockDim x 2 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]
-        // [bidx: n_slots x 4 B]; shading records (bmat) stay in global memory
-        // (L1/L2-resident, read once per hit).
-        S.base = (__attribute__((address_space(3))) uint16_t*)reinterpret_cast<uint16_t*>(smem) + threadIdx.x;
+        // [stacks: stack_cap x blockDim x 4 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]
+        // [bidx: n_slots x 4 B][leaves: n_leaves x 4 B]; shading records (bmat) stay
+        // in global memory (L1/L2-resident, read once per hit).
+        S.base = (__attribute__((address_space(3))) uint32_t*)reinterpret_cast<uint32_t*>(smem) + threadIdx.x;
         double4* scene = smem + bvh_stack_bytes(p.stack_cap) / sizeof(double4);
         if constexpr (kLDS) {
             double4* lds_nodes = scene;
             double4* lds_geo = scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4));
             int32_t* lds_idx = reinterpret_cast<int32_t*>(lds_geo + p.n_slots);
+            int32_t* lds_leaves = lds_idx + p.n_slots;
             const double4* gn = reinterpret_cast<const double4*>(p.nodes);
             const int n4 = p.n_nodes * (int)(sizeof(Bvh4Node) / sizeof(double4));
             for (int i = threadIdx.x; i < n4; i += blockDim.x) lds_nodes[i] = gn[i];
@@ -714,9 +736,11 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 lds_geo[i] = p.bgeo[i];
                 lds_idx[i] = p.bidx[i];
             }
+            for (int i = threadIdx.x; i < p.n_leaves; i += blockDim.x) lds_leaves[i] = p.leaves[i];
             sv.nodes = reinterpret_cast<const Bvh4Node*>(lds_nodes);
             sv.bgeo = lds_geo;
             sv.bidx = lds_idx;
+            sv.leaves = lds_leaves;
         }
     } else if constexpr (kLDS) {
         for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
@@ -731,6 +755,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     Trav T;
     uint32_t state = kIdleState;
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
+    uint32_t next_chunk = 0;                // lane 0: the wave's next chunk, fetched ahead
+    if (lane == 0) next_chunk = atomicAdd(p.queue, 1u);
     bool exhausted = false;
 #ifdef TRAY_PROFILE
     uint64_t prof[16] = {};
@@ -742,15 +768,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         // Refill idle lanes from the wave's pool, fetching 64-item chunks from the global queue.
         PROF_T0();
         uint64_t idle = __ballot(!L.busy);
+        if (__popcll(idle) < TRAY_REFILL_BATCH && idle != ~0ull) idle = 0ull;  // batch refills
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
-                uint32_t c = 0;
-                if (lane == 0) c = atomicAdd(p.queue, 1u);
-                c = __shfl(c, 0);
+                const uint32_t c = __shfl(next_chunk, 0);
                 if (c >= p.nchunks) {
                     exhausted = true;
                     break;
                 }
+                if (lane == 0) next_chunk = atomicAdd(p.queue, 1u);  // prefetch the one after
                 pool_next = c * 64u;
                 pool_end = pool_next + 64u;
             }
@@ -813,7 +839,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 PROF_CNT(7, __popcll(m_leaf));
                 if (state == kLeafState) {
                     uint32_t tested;
-                    state = trav_leaf(T, sv, L.org, L.dir, tested);
+                    state = trav_leaf(T, sv, S, L.org, L.dir, tested);
                     if constexpr (kStats) st.spheres += tested;
                 }
                 PROF_ADD(2);
@@ -872,7 +898,16 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
     if (!decode_item(p, q * (uint32_t)p.spp, x, j, s0)) return;
     const double* smp = p.samples + (size_t)q * (size_t)p.spp * 3;
     D3 sum = d3(0, 0, 0);
-    for (int32_t s = 0; s < p.spp; ++s) sum = add(sum, d3(smp[3 * s], smp[3 * s + 1], smp[3 * s + 2]));
+    // Loads of 8 samples are issued together; the adds stay in sample order.
+    int32_t s = 0;
+    for (; s + 8 <= p.spp; s += 8) {
+        double v[24];
+#pragma unroll
+        for (int k = 0; k < 24; ++k) v[k] = smp[3 * s + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum = add(sum, d3(v[3 * k], v[3 * k + 1], v[3 * k + 2]));
+    }
+    for (; s < p.spp; ++s) sum = add(sum, d3(smp[3 * s], smp[3 * s + 1], smp[3 * s + 2]));
     const double inv = 1.0 / (double)p.spp;  // colorSumDiv (ray/tracer.go:123)
     const D3 mean = smul(sum, inv);
     const size_t off = (size_t)j * (size_t)p.width + (size_t)x;
@@ -923,9 +958,9 @@ static int resident_blocks(int device, KernelFn fn, int threads, size_t lds) {
     return cus * per_cu;
 }
 
-size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t stack_cap) {
+size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap) {
     return kUniformsBytes + bvh_stack_bytes(stack_cap) + (size_t)n_nodes * sizeof(Bvh4Node) +
-           (size_t)n_slots * (sizeof(double4) + sizeof(int32_t));
+           (size_t)n_slots * (sizeof(double4) + sizeof(int32_t)) + (size_t)n_leaves * sizeof(int32_t);
 }
 
 // Bands of 8-row tile rows, each <= kMaxBandSamples samples (at least one tile row).
@@ -948,13 +983,15 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (p.rows <= 0) return hipSuccess;
     if (!band_fits(p.width, p.spp)) return hipErrorInvalidValue;
     p.tiles_x = (p.width + 7) / 8;
+    p.inv_spp = 1.0 / (double)p.spp;
+    p.inv_tiles_x = 1.0 / (double)p.tiles_x;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     bool use_lds;
     size_t lds;
     if (use_bvh) {
-        const size_t full = bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.stack_cap);
+        const size_t full = bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap);
         use_lds = full <= kMaxLDSBytes;
         lds = use_lds ? (full + 15) / 16 * 16 : kUniformsBytes + bvh_stack_bytes(p.stack_cap);
         if (lds > kMaxLDSBytes) return hipErrorInvalidValue;  // stack bound checked when the scene is built

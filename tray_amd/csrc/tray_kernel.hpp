@@ -53,12 +53,14 @@ struct KernelParams {
     uint32_t nchunks;    // 64-item chunks of the band's work items (one item = one sample)
     uint32_t items;      // band work items: 8x8-tile-padded pixels x spp
     int32_t j0, band_rows;  // the band: compact rows [j0, j0 + band_rows)
+    double inv_spp, inv_tiles_x;  // RN(1/spp), RN(1/tiles_x): item decoding
     double* samples;     // per-item path colours (3 doubles), summed in order by the resolve kernel
     const Bvh4Node* nodes;  // exact-culling 4-wide BVH (tray_bvh.cpp), root first
+    const int32_t* leaves;  // per leaf: (first slot << 3) | count
     const double4* bgeo;    // spheres in leaf-slot order
     const int32_t* bidx;    // original index per slot
     const MatRec* bmat;     // shading record per slot
-    int32_t n_nodes, n_slots;
+    int32_t n_nodes, n_slots, n_leaves;
     int32_t stack_cap;      // traversal stack slots per lane (Bvh::stack_max + 1)
     unsigned long long* stats;  // nullable: [segments, sphere tests, box tests]
     int32_t width, height, spp, max_depth;
@@ -84,7 +86,7 @@ bool band_fits(int32_t width, int32_t spp);
 
 // LDS the BVH kernel needs to hold the whole BVH scene (plus its traversal
 // stacks) on chip; above kMaxLDSBytes it reads the scene from global memory.
-size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t stack_cap);
+size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap);
 
 // Padded geometry length for n spheres (see KernelParams::geo).
 inline int32_t padded_spheres(int32_t n) { return ((n + 3) / 4) * 4 + 4; }
