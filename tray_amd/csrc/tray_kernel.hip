@@ -8,20 +8,18 @@
 // RandomUnitVector/InDisc samplers (ray/rand.go:30-32, via include/tray.h's
 // counter RNG).
 //
-// Execution model (one launch per row set):
-//   * one lane = one pixel; the lane runs all r samples of its pixel in order,
-//     so the per-pixel sum has the reference's summation order
-//     (ray/tracer.go:143) and needs no atomics;
-//   * the recursion of RayColor becomes an iterative bounce loop with PATH
-//     REGENERATION: when a lane's path ends it immediately starts its next
-//     sample, so a wave iterates max-over-lanes(total segments) times instead of
-//     sum-over-samples(max segments). The wave leaves the loop when a __ballot
-//     of unfinished lanes is empty;
-//   * the sphere geometry (cx, cy, cz, R*R: 32 B/sphere) is staged once per
-//     workgroup into LDS and read by wave-uniform broadcast ds_read_b128;
-//     materials are fetched from global memory only for the closest hit;
-//   * a workgroup is 4 waves covering a 16x16 pixel tile (8x8 per wave), so a
-//     wave's primary rays are coherent.
+// Execution model (per launch band of rows):
+//   * a work item is one sample (pixel, s); a lane traces one path at a time and
+//     stores its colour in the band's sample buffer; resolve_kernel then adds
+//     each pixel's samples in sample order (ray/tracer.go:143) and scales by 1/r;
+//   * the recursion of RayColor becomes an iterative bounce loop; lanes refill
+//     individually from a persistent work queue, so a wave never waits for its
+//     slowest path;
+//   * Scene.Hit is an exact-culling 4-wide BVH (tray_bvh.cpp) staged in LDS,
+//     one 1024-lane workgroup per CU; each lane is a state machine (refill /
+//     node visit / leaf / shade) and the expensive phases run batched;
+//   * small scenes, or TRAY_FLAG_LINEAR_SCAN, use the reference-order linear
+//     scan over NaN-padded LDS geometry instead.
 // Arithmetic: FP64, reference op order, compiled with -ffp-contract=off.
 // The one intentional difference from the Go recursion: attenuations are
 // multiplied outer-first (((att0*att1)*att2)*sky instead of
