@@ -192,6 +192,20 @@ int tray_scene_upload(const tray_sphere *spheres, int32_t n_spheres, const tray_
                       int32_t device, tray_scene_t *out);
 int tray_scene_release(tray_scene_t scene);
 
+/* How an uploaded scene is traversed (diagnostics; no reference counterpart). */
+typedef struct tray_scene_info {
+    int32_t n_spheres;
+    int32_t has_bvh;      /* 0: every render uses the reference-order linear scan */
+    int32_t leaf_max;     /* spheres per BVH leaf (1 unless the scene must shrink to fit LDS) */
+    int32_t n_nodes;      /* 4-wide BVH nodes */
+    int32_t n_leaves;
+    int32_t stack_depth;  /* traversal stack bound (entries) */
+    int32_t lds_resident; /* 1: nodes + geometry are staged in LDS; 0: read from global memory */
+    int32_t reserved;
+    double bound;         /* M: the BVH needs every ray origin in [-M, M]^3 */
+} tray_scene_info;
+int tray_scene_get_info(tray_scene_t scene, tray_scene_info *out);
+
 /* Asynchronous render into DEVICE memory on `stream` (a hipStream_t, or NULL for
  * the null stream of the scene's device). out_device: compact rows in the
  * params->output format; segments_device nullable. Returns after enqueueing. */

@@ -168,3 +168,9 @@ def test_scene_flattening_errors():
         ray.Scene([Weird()]).to_array()
     arr = ray.Scene([ray.Sphere((0, 0, -1), 0.5, ray.Metal((0.8, 0.8, 0.8), 0.3))]).to_array()
     assert arr["material"][0] == _lib.METAL and arr["param"][0] == 0.3
+
+
+def test_scene_info_layout(L):
+    import ctypes
+
+    assert ctypes.sizeof(L.SceneInfo) == 8 * 4 + 8

@@ -260,3 +260,58 @@ def test_stats_counters(L, O):
         else:
             assert 0 < sph < seg * len(sc) and box > 0
     dev.release()
+
+
+def test_scene_info_and_traversal_paths(L, O):
+    """The book scene is an LDS-resident 1-sphere-per-leaf BVH; a scene too big
+    for LDS traverses from global memory; both equal the linear scan."""
+    book = L.DeviceScene(O.rich_scene(2), bg_struct(L, DEFAULT_BG), 0)
+    i = book.info()
+    assert (i.n_spheres, i.has_bvh, i.leaf_max, i.lds_resident) == (486, 1, 1, 1)
+    assert 0 < i.stack_depth <= 48 and i.n_leaves == 486 and i.bound == 2000.0  # ground: y in [-2000, 0]
+    big = O.rich_scene(5, 40)
+    ib = L.DeviceScene(big, bg_struct(L, DEFAULT_BG), 0).info()
+    assert ib.has_bvh == 1 and ib.lds_resident == 0
+    tiny = L.DeviceScene(O.default_scene(), bg_struct(L, DEFAULT_BG), 0).info()
+    assert tiny.has_bvh == 0
+    st = camera(L, RICH_SETUP, 40, 24)
+    bvh, sb = gpu_render(L, big, DEFAULT_BG, st, 40, 24, 2, 20, 0.5, 8)
+    lin, sl = gpu_render(L, big, DEFAULT_BG, st, 40, 24, 2, 20, 0.5, 8, flags=L.FLAG_LINEAR_SCAN)
+    assert np.array_equal(sb, sl) and np.array_equal(bvh, lin)
+
+
+def test_bvh_deep_tree(L, O):
+    """Spheres shrinking geometrically along a line (SAH peels them one by one):
+    a deep tree, bounded by median splits, with a deep traversal stack."""
+    from oracle.oracle import SPHERE_DTYPE
+
+    n = 160
+    s = np.zeros(n, dtype=SPHERE_DTYPE)
+    x = np.cumsum(0.97 ** np.arange(n))
+    s["center"][:, 0] = x - x.mean()
+    s["center"][:, 1] = 0.3 * np.sin(np.arange(n))
+    s["radius"] = 0.45 * 0.97 ** np.arange(n)
+    s["material"] = 1 + np.arange(n) % 3
+    s["albedo"] = 0.7
+    s["param"] = np.where(s["material"] == 3, 1.5, 0.2)
+    dev = L.DeviceScene(s, bg_struct(L, DEFAULT_BG), 0)
+    assert dev.info().has_bvh == 1
+    setup = np.array([0.0, 2.0, 14.0, 0, 0, 0, 0, 1, 0, 60.0, 1.0, 14.0, 0.0])
+    st = camera(L, setup, 96, 32)
+    bvh, sb = gpu_render(L, s, DEFAULT_BG, st, 96, 32, 2, 30, 0.5, 12)
+    lin, sl = gpu_render(L, s, DEFAULT_BG, st, 96, 32, 2, 30, 0.5, 12, flags=L.FLAG_LINEAR_SCAN)
+    assert np.array_equal(sb, sl) and np.array_equal(bvh, lin)
+
+
+def test_launch_bands_are_invisible(L, O, monkeypatch):
+    """A frame split into several launch bands (small TRAY_BAND_SAMPLES) renders
+    the same bits as one band, tiled and untiled."""
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, 72, 41)
+    one, s1 = gpu_render(L, sc, DEFAULT_BG, st, 72, 41, 3, 20, 0.5, 4)
+    monkeypatch.setenv("TRAY_BAND_SAMPLES", str(72 * 8 * 3 * 2))  # two 8-row tile rows per band
+    many, sm = gpu_render(L, sc, DEFAULT_BG, st, 72, 41, 3, 20, 0.5, 4)
+    assert np.array_equal(s1, sm) and np.array_equal(one, many)
+    t, stl = gpu_render(L, sc, DEFAULT_BG, st, 72, 41, 3, 20, 0.5, 4, tile_rows=8, tile_count=2, tile_index=1)
+    rows = [y for y in range(41) if (y // 8) % 2 == 1]
+    assert np.array_equal(t, one[rows]) and np.array_equal(stl, s1[rows])

@@ -100,6 +100,13 @@ class Params(ctypes.Structure):
 FLAG_LINEAR_SCAN = 1  # TRAY_FLAG_LINEAR_SCAN
 
 
+class SceneInfo(ctypes.Structure):
+    """tray_scene_info: how an uploaded scene is traversed."""
+    _fields_ = [("n_spheres", ctypes.c_int32), ("has_bvh", ctypes.c_int32), ("leaf_max", ctypes.c_int32),
+                ("n_nodes", ctypes.c_int32), ("n_leaves", ctypes.c_int32), ("stack_depth", ctypes.c_int32),
+                ("lds_resident", ctypes.c_int32), ("reserved", ctypes.c_int32), ("bound", ctypes.c_double)]
+
+
 class TrayError(RuntimeError):
     def __init__(self, code: int, message: str):
         super().__init__(f"tray error {code}: {message}")
@@ -121,6 +128,7 @@ EXPORTS = (
     "tray_render",
     "tray_scene_upload",
     "tray_scene_release",
+    "tray_scene_get_info",
     "tray_render_async",
     "tray_render_stats_async",
     "tray_params_rows",
@@ -157,6 +165,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
                               ctypes.POINTER(Params), i32, vp, u32p]
     L.tray_scene_upload.argtypes = [vp, i32, ctypes.POINTER(Background), i32, ctypes.POINTER(vp)]
     L.tray_scene_release.argtypes = [vp]
+    L.tray_scene_get_info.argtypes = [vp, ctypes.POINTER(SceneInfo)]
     L.tray_render_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
     L.tray_render_stats_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
     L.tray_params_rows.argtypes = [ctypes.POINTER(Params)]
@@ -214,7 +223,8 @@ def render(spheres, background: Background, camera: CameraState, params: Params,
 
 class DeviceScene:
     """A scene uploaded once to one device (tray_scene_upload); render many times.
-    Renders of one DeviceScene must be ordered on one stream (shared work queue)."""
+    Renders of one DeviceScene must be ordered on one stream (shared work queue and
+    sample buffer)."""
 
     def __init__(self, spheres, background: Background, device: int = 0, lib_path: str | None = None):
         self.L = lib(lib_path)
@@ -242,6 +252,13 @@ class DeviceScene:
                                             stats_ptr, stream)
         if rc != TRAY_OK:
             raise TrayError(rc, self.L.tray_last_error().decode())
+
+    def info(self) -> SceneInfo:
+        out = SceneInfo()
+        rc = self.L.tray_scene_get_info(self.handle, ctypes.byref(out))
+        if rc != TRAY_OK:
+            raise TrayError(rc, self.L.tray_last_error().decode())
+        return out
 
     def release(self) -> None:
         if self.handle:

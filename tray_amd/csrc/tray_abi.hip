@@ -102,7 +102,7 @@ struct tray_scene_s {
     // exact-culling BVH (absent for tiny or non-finite scenes)
     bool has_bvh;
     double bvh_bound;
-    int32_t n_nodes, n_slots, n_leaves, stack_cap;
+    int32_t n_nodes, n_slots, n_leaves, stack_cap, leaf_max;
     tray::Bvh4Node* nodes;
     int32_t* leaves;
     double4* bgeo;
@@ -242,6 +242,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->n_leaves = (int32_t)bvh.leaves.size();
     sc->leaves = nullptr;
     sc->stack_cap = bvh.stack_max + 1;
+    sc->leaf_max = has_bvh ? bvh.leaf_max : 0;
     sc->nodes = nullptr;
     sc->bgeo = nullptr;
     sc->bidx = nullptr;
@@ -296,6 +297,23 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         return hip_fail(e, "scene upload");
     }
     *out = sc;
+    return TRAY_OK;
+}
+
+int tray_scene_get_info(tray_scene_t sc, tray_scene_info* out) {
+    if (!sc || !out) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+    memset(out, 0, sizeof(*out));
+    out->n_spheres = sc->n;
+    out->has_bvh = sc->has_bvh ? 1 : 0;
+    out->leaf_max = sc->leaf_max;
+    out->n_nodes = sc->n_nodes;
+    out->n_leaves = sc->n_leaves;
+    out->stack_depth = sc->has_bvh ? sc->stack_cap - 1 : 0;
+    out->lds_resident = sc->has_bvh && bvh_scene_lds_bytes(sc->n_nodes, sc->n_slots, sc->n_leaves, sc->stack_cap) <=
+                                           kMaxLDSBytes
+                            ? 1
+                            : 0;
+    out->bound = sc->bvh_bound;
     return TRAY_OK;
 }
 

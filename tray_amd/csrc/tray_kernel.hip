@@ -28,6 +28,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -325,8 +326,19 @@ __device__ __forceinline__ float f32_up(double v) {
 // Lane states of the BVH kernel.
 enum : uint32_t { kIdleState = 0, kTravState = 1, kLeafState = 2, kShadeState = 3 };
 
+// 1: slab distances of two children per packed FMA (v_pk_fma_f32).
+#ifndef TRAY_PK_FMA
+#define TRAY_PK_FMA 0
+#endif
+typedef float tray_f2 __attribute__((ext_vector_type(2)));
+typedef float tray_f4 __attribute__((ext_vector_type(4)));
+
 struct Trav {
+#if TRAY_PK_FMA
+    tray_f2 ixv, iyv, izv, oxv, oyv, ozv;  // FP32 ray, each value twice: t = box * inv - org * inv
+#else
     float ix, iy, iz, oix, oiy, oiz;  // FP32 ray: t = box * inv - org * inv
+#endif
     float tlim;                       // closest rounded up to float
     int32_t near_x, near_y, near_z;   // byte offsets of the near planes in a node
     uint32_t cur;                     // child reference to visit next (kBvhNone: done)
@@ -377,16 +389,25 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
     if (__builtin_fabsf(dyf) < 1e-30f) dyf = 1e-30f;
     if (__builtin_fabsf(dzf) < 1e-30f) dzf = 1e-30f;
     // ~1 ulp reciprocal: inside the padding's error budget (tray_bvh.cpp)
-    T.ix = __builtin_amdgcn_rcpf(dxf);
-    T.iy = __builtin_amdgcn_rcpf(dyf);
-    T.iz = __builtin_amdgcn_rcpf(dzf);
-    T.oix = (float)org.x * T.ix;
-    T.oiy = (float)org.y * T.iy;
-    T.oiz = (float)org.z * T.iz;
+    const float ix = __builtin_amdgcn_rcpf(dxf);
+    const float iy = __builtin_amdgcn_rcpf(dyf);
+    const float iz = __builtin_amdgcn_rcpf(dzf);
+    const float oix = (float)org.x * ix, oiy = (float)org.y * iy, oiz = (float)org.z * iz;
+#if TRAY_PK_FMA
+    T.ixv = tray_f2{ix, ix};
+    T.iyv = tray_f2{iy, iy};
+    T.izv = tray_f2{iz, iz};
+    T.oxv = tray_f2{-oix, -oix};
+    T.oyv = tray_f2{-oiy, -oiy};
+    T.ozv = tray_f2{-oiz, -oiz};
+#else
+    T.ix = ix, T.iy = iy, T.iz = iz;
+    T.oix = oix, T.oiy = oiy, T.oiz = oiz;
+#endif
     // Bvh4Node::box[a][s]: the near plane is the low one when the ray runs up the axis.
-    T.near_x = T.ix < 0.0f ? 16 : 0;
-    T.near_y = T.iy < 0.0f ? 48 : 32;
-    T.near_z = T.iz < 0.0f ? 80 : 64;
+    T.near_x = ix < 0.0f ? 16 : 0;
+    T.near_y = iy < 0.0f ? 48 : 32;
+    T.near_z = iz < 0.0f ? 80 : 64;
 }
 
 // Push `key` if valid. The store is unconditional: with no push it writes
@@ -412,10 +433,6 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stack& S, uint32_t 
     return kBvhNone;
 }
 
-// 1: slab distances of two children per packed FMA (v_pk_fma_f32).
-#ifndef TRAY_PK_FMA
-#define TRAY_PK_FMA 0
-#endif
 
 // One node visit: test the four child boxes, visit the nearest hit child next
 // (an inner node or a leaf) and push the other hit children far-to-near.
@@ -433,15 +450,14 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
     const uint32_t below = S.base[max(T.sp - 1, 0) * kBvhBlock];  // read ahead for a pop
     const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
 #if TRAY_PK_FMA
-    typedef float tray_f2 __attribute__((ext_vector_type(2)));
-    const tray_f2 ixv = {T.ix, T.ix}, iyv = {T.iy, T.iy}, izv = {T.iz, T.iz};
-    const tray_f2 oxv = {-T.oix, -T.oix}, oyv = {-T.oiy, -T.oiy}, ozv = {-T.oiz, -T.oiz};
-#define TRAY_PK(v, iv, ov, lo, hi) \
-    const tray_f2 lo = __builtin_elementwise_fma(tray_f2{v.x, v.y}, iv, ov), hi = __builtin_elementwise_fma(tray_f2{v.z, v.w}, iv, ov);
-    TRAY_PK(nx, ixv, oxv, tnx01, tnx23) TRAY_PK(fx, ixv, oxv, tfx01, tfx23)
-    TRAY_PK(ny, iyv, oyv, tny01, tny23) TRAY_PK(fy, iyv, oyv, tfy01, tfy23)
-    TRAY_PK(nz, izv, ozv, tnz01, tnz23) TRAY_PK(fz, izv, ozv, tfz01, tfz23)
+#define TRAY_PK(off, iv, ov, A, B)                                       \
+    const tray_f4 A##_v = *reinterpret_cast<const tray_f4*>(nb + (off)); \
+    const tray_f2 A = __builtin_elementwise_fma(A##_v.lo, iv, ov), B = __builtin_elementwise_fma(A##_v.hi, iv, ov);
+    TRAY_PK(T.near_x, T.ixv, T.oxv, tnx01, tnx23) TRAY_PK(T.near_x ^ 16, T.ixv, T.oxv, tfx01, tfx23)
+    TRAY_PK(T.near_y, T.iyv, T.oyv, tny01, tny23) TRAY_PK(T.near_y ^ 16, T.iyv, T.oyv, tfy01, tfy23)
+    TRAY_PK(T.near_z, T.izv, T.ozv, tnz01, tnz23) TRAY_PK(T.near_z ^ 16, T.izv, T.ozv, tfz01, tfz23)
 #undef TRAY_PK
+    (void)nx, (void)fx, (void)ny, (void)fy, (void)nz, (void)fz;
     const float tnx[4] = {tnx01.x, tnx01.y, tnx23.x, tnx23.y}, tfx[4] = {tfx01.x, tfx01.y, tfx23.x, tfx23.y};
     const float tny[4] = {tny01.x, tny01.y, tny23.x, tny23.y}, tfy[4] = {tfy01.x, tfy01.y, tfy23.x, tfy23.y};
     const float tnz[4] = {tnz01.x, tnz01.y, tnz23.x, tnz23.y}, tfz[4] = {tfz01.x, tfz01.y, tfz23.x, tfz23.y};
@@ -961,10 +977,19 @@ size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, i
            (size_t)n_slots * (sizeof(double4) + sizeof(int32_t)) + (size_t)n_leaves * sizeof(int32_t);
 }
 
-// Bands of 8-row tile rows, each <= kMaxBandSamples samples (at least one tile row).
+uint64_t max_band_samples() {
+    const char* e = getenv("TRAY_BAND_SAMPLES");
+    if (e && *e) {
+        const unsigned long long v = strtoull(e, nullptr, 10);
+        if (v > 0 && v < kMaxBandSamples) return v;
+    }
+    return kMaxBandSamples;
+}
+
+// Bands of 8-row tile rows, each <= max_band_samples() samples (at least one tile row).
 static int32_t band_tile_rows(int32_t width, int32_t spp) {
     const uint64_t per = (uint64_t)((width + 7) / 8) * 64u * (uint64_t)spp;
-    return (int32_t)std::max<uint64_t>(1, kMaxBandSamples / per);
+    return (int32_t)std::max<uint64_t>(1, max_band_samples() / per);
 }
 
 size_t sample_buffer_bytes(int32_t width, int32_t rows, int32_t spp) {

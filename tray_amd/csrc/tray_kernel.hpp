@@ -77,8 +77,10 @@ struct KernelParams {
 
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
 
-// Samples per launch band (the sample buffer holds one band: 24 B per sample).
+// Samples per launch band (the sample buffer holds one band: 24 B per sample);
+// the TRAY_BAND_SAMPLES environment variable lowers it (tests exercise bands).
 constexpr uint64_t kMaxBandSamples = 1ull << 26;
+uint64_t max_band_samples();
 // Bytes of sample buffer launch_render needs for `rows` compact rows.
 size_t sample_buffer_bytes(int32_t width, int32_t rows, int32_t spp);
 // False when one 8-row band has more than 2^31 samples (item indices are 32-bit).
