@@ -315,3 +315,14 @@ def test_launch_bands_are_invisible(L, O, monkeypatch):
     t, stl = gpu_render(L, sc, DEFAULT_BG, st, 72, 41, 3, 20, 0.5, 4, tile_rows=8, tile_count=2, tile_index=1)
     rows = [y for y in range(41) if (y // 8) % 2 == 1]
     assert np.array_equal(t, one[rows]) and np.array_equal(stl, s1[rows])
+
+
+def test_stack_overflow_area(L, O, monkeypatch):
+    """Traversal-stack slots beyond the LDS ones live in a global overflow area:
+    forcing the minimum of LDS slots renders the same bits."""
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, 64, 36)
+    a, sa = gpu_render(L, sc, DEFAULT_BG, st, 64, 36, 4, 50, 0.5, 3)
+    monkeypatch.setenv("TRAY_STACK_LDS_SLOTS", "8")
+    b, sb = gpu_render(L, sc, DEFAULT_BG, st, 64, 36, 4, 50, 0.5, 3)
+    assert np.array_equal(sa, sb) and np.array_equal(a, b)

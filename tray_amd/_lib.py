@@ -165,7 +165,8 @@ def lib(path: str | None = None) -> ctypes.CDLL:
                               ctypes.POINTER(Params), i32, vp, u32p]
     L.tray_scene_upload.argtypes = [vp, i32, ctypes.POINTER(Background), i32, ctypes.POINTER(vp)]
     L.tray_scene_release.argtypes = [vp]
-    L.tray_scene_get_info.argtypes = [vp, ctypes.POINTER(SceneInfo)]
+    if hasattr(L, "tray_scene_get_info"):  # absent from builds older than this binding (A/B tools)
+        L.tray_scene_get_info.argtypes = [vp, ctypes.POINTER(SceneInfo)]
     L.tray_render_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
     L.tray_render_stats_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
     L.tray_params_rows.argtypes = [ctypes.POINTER(Params)]

@@ -105,6 +105,7 @@ struct tray_scene_s {
     int32_t n_nodes, n_slots, n_leaves, stack_cap, leaf_max;
     tray::Bvh4Node* nodes;
     int32_t* leaves;
+    uint32_t* stack_ovf;  // traversal-stack slots beyond LDS (deep BVHs only)
     double4* bgeo;
     int32_t* bidx;
     tray::MatRec* bmat;
@@ -241,6 +242,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->n_slots = (int32_t)bvh.geo.size();
     sc->n_leaves = (int32_t)bvh.leaves.size();
     sc->leaves = nullptr;
+    sc->stack_ovf = nullptr;
     sc->stack_cap = bvh.stack_max + 1;
     sc->leaf_max = has_bvh ? bvh.leaf_max : 0;
     sc->nodes = nullptr;
@@ -269,6 +271,8 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess && has_bvh) {
         e = hipMalloc(&sc->nodes, sizeof(Bvh4Node) * bvh.nodes.size());
+        const size_t ovf = bvh_stack_overflow_bytes(bvh.stack_max + 1, device);
+        if (e == hipSuccess && ovf) e = hipMalloc(&sc->stack_ovf, ovf);
         if (e == hipSuccess) e = hipMalloc(&sc->leaves, sizeof(int32_t) * bvh.leaves.size());
         if (e == hipSuccess)
             e = hipMemcpy(sc->leaves, bvh.leaves.data(), sizeof(int32_t) * bvh.leaves.size(), hipMemcpyHostToDevice);
@@ -290,6 +294,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         (void)hipFree(sc->queue);
         (void)hipFree(sc->nodes);
         (void)hipFree(sc->leaves);
+        (void)hipFree(sc->stack_ovf);
         (void)hipFree(sc->bgeo);
         (void)hipFree(sc->bidx);
         (void)hipFree(sc->bmat);
@@ -325,6 +330,7 @@ int tray_scene_release(tray_scene_t sc) {
     if (sc->queue) (void)hipFree(sc->queue);
     if (sc->nodes) (void)hipFree(sc->nodes);
     if (sc->leaves) (void)hipFree(sc->leaves);
+    if (sc->stack_ovf) (void)hipFree(sc->stack_ovf);
     if (sc->bgeo) (void)hipFree(sc->bgeo);
     if (sc->bidx) (void)hipFree(sc->bidx);
     if (sc->bmat) (void)hipFree(sc->bmat);
@@ -378,6 +384,7 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.n_slots = sc->n_slots;
     k.n_leaves = sc->n_leaves;
     k.leaves = sc->leaves;
+    k.stack_ovf = sc->stack_ovf;
     k.stack_cap = sc->stack_cap;
     // The BVH's conservative FP32 box test assumes every ray origin lies within
     // [-M, M]^3 (tray_bvh.cpp): hit points do; check the camera and lens disc.

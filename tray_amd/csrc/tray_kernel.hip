@@ -356,14 +356,43 @@ struct Trav {
 // the scene); the linear scan runs 256-lane workgroups.
 constexpr int kBvhBlock = 256 * TRAY_BVH_WAVES_PER_SIMD;
 static_assert(kBvhBlock <= 1024, "BVH workgroup larger than 1024 lanes");
+// Traversal stack slots per lane are kept in LDS as far as the workgroup's LDS
+// allows after the scene (4 KB per slot), at least kStackLdsMin of them.
+constexpr int32_t kStackLdsMin = 8;
+constexpr size_t kStackSlotBytes = (size_t)kBvhBlock * sizeof(uint32_t);
 
-// Per-lane traversal stack of sort keys in LDS, slot i of the lane at
-// base[i * kBvhBlock] (consecutive lanes, consecutive banks). The top entry
-// lives in Trav::top and slot i >= 1 holds the entry below the i-th; slot 0 is
-// a scratch slot, so pushes need no branches (stack_cap = depth + 1).
+// Per-lane traversal stack of sort keys. The top entry lives in Trav::top and
+// slot i >= 1 holds the entry below the i-th; slot 0 is a scratch slot, so
+// pushes need no branches (stack_cap = depth bound + 1). Slots below `lds`
+// are in LDS, slot i of the lane at base[i * kBvhBlock] (consecutive lanes,
+// consecutive banks); a scene whose bound is deeper keeps the rest in a global
+// overflow area (spill set: one wave-uniform branch per access otherwise).
+template <bool kSpill>
 struct Stack {
+    static constexpr bool spill = kSpill;
     __attribute__((address_space(3))) uint32_t* base;  // this lane's slot 0
+    uint32_t* ovf;     // this lane's slot `lds` in the overflow area (stride: grid lanes)
+    uint32_t stride;
+    int32_t lds;
 };
+
+template <class Stk>
+__device__ __forceinline__ uint32_t stack_load(const Stk& S, int32_t i) {
+    if constexpr (Stk::spill)
+        if (i >= S.lds) return S.ovf[(size_t)(i - S.lds) * S.stride];
+    return S.base[i * kBvhBlock];
+}
+
+template <class Stk>
+__device__ __forceinline__ void stack_store(const Stk& S, int32_t i, uint32_t v) {
+    if constexpr (Stk::spill) {
+        if (i >= S.lds) {
+            S.ovf[(size_t)(i - S.lds) * S.stride] = v;
+            return;
+        }
+    }
+    S.base[i * kBvhBlock] = v;
+}
 
 // Sort key of a hit child: the upper 16 bits of its entry distance (tn >= 0, so
 // keys order like distances, to bf16 precision, and never exceed the true tn)
@@ -412,9 +441,10 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
 
 // Push `key` if valid. The store is unconditional: with no push it writes
 // slot sp, above the stack.
-__device__ __forceinline__ void stack_push(Trav& T, const Stack& S, uint32_t key) {
+template <class Stk>
+__device__ __forceinline__ void stack_push(Trav& T, const Stk& S, uint32_t key) {
     const bool valid = key != ~0u;
-    S.base[T.sp * kBvhBlock] = T.top;
+    stack_store(S, T.sp, T.top);
     T.top = valid ? key : T.top;
     T.sp += valid ? 1 : 0;
 }
@@ -422,13 +452,14 @@ __device__ __forceinline__ void stack_push(Trav& T, const Stack& S, uint32_t key
 // Pop entries until one whose box may still hold a closer hit (key_tn <= tlim:
 // the test of the box against the current closest hit, as at push time); its
 // reference, or kBvhNone. `below` = slot sp - 1, read ahead.
-__device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stack& S, uint32_t below) {
+template <class Stk>
+__device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t below) {
     while (T.sp > 0) {
         const uint32_t key = T.top;
         --T.sp;
         T.top = below;
         if (key_tn(key) <= T.tlim) return key & 0xFFFFu;
-        if (T.sp > 0) below = S.base[(T.sp - 1) * kBvhBlock];
+        if (T.sp > 0) below = stack_load(S, T.sp - 1);
     }
     return kBvhNone;
 }
@@ -437,7 +468,8 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stack& S, uint32_t 
 // One node visit: test the four child boxes, visit the nearest hit child next
 // (an inner node or a leaf) and push the other hit children far-to-near.
 // Returns the new lane state.
-__device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, const Stack& S, uint32_t& tested) {
+template <class Stk>
+__device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, const Stk& S, uint32_t& tested) {
     const char* nb = reinterpret_cast<const char*>(sv.nodes + T.cur);
     // Near and far planes of the four children on each axis (far = near ^ 16).
     const float4 nx = *reinterpret_cast<const float4*>(nb + T.near_x);
@@ -447,7 +479,7 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
     const float4 nz = *reinterpret_cast<const float4*>(nb + T.near_z);
     const float4 fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ 16));
     const uint4 rf = *reinterpret_cast<const uint4*>(nb + 96);
-    const uint32_t below = S.base[max(T.sp - 1, 0) * kBvhBlock];  // read ahead for a pop
+    const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for a pop
     const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
 #if TRAY_PK_FMA
 #define TRAY_PK(off, iv, ov, A, B)                                       \
@@ -506,9 +538,10 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
 }
 
 // Test the spheres of leaf T.cur (FP64, any-order rule), then pop the next entry.
-__device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const Stack& S, const D3& org,
+template <class Stk>
+__device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const Stk& S, const D3& org,
                                               const D3& dir, uint32_t& tested) {
-    const uint32_t below = S.base[max(T.sp - 1, 0) * kBvhBlock];  // read ahead for the pop
+    const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for the pop
     const int32_t info = sv.leaves[T.cur & (kBvhLeafBit - 1u)];
     const int32_t first = info >> 3, end = first + (info & 7);
     tested = 0;
@@ -700,12 +733,10 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 // wave's slowest ray: it shades and starts its next segment while others still
 // traverse.
 
-// LDS stack bytes of a BVH workgroup (32-bit entries).
-__host__ __device__ constexpr size_t bvh_stack_bytes(int32_t stack_cap) {
-    return (size_t)stack_cap * kBvhBlock * sizeof(uint32_t);
-}
+// LDS bytes of `slots` stack slots of a BVH workgroup (32-bit entries).
+__host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (size_t)slots * kStackSlotBytes; }
 
-template <bool kLDS, bool kBVH, bool kStats>
+template <bool kLDS, bool kBVH, bool kStats, bool kSpill>
 __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
     extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
     __attribute__((address_space(3))) Uniforms* uni_lds =
@@ -731,13 +762,16 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     }
     const UniPtr uni = uni_lds;
     SceneView sv{p.geo, p.nodes, p.leaves, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
-    Stack S{nullptr};
+    Stack<kSpill> S{nullptr, nullptr, 0, 0};
     if constexpr (kBVH) {
         // [stacks: stack_cap x blockDim x 4 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]
         // [bidx: n_slots x 4 B][leaves: n_leaves x 4 B]; shading records (bmat) stay
         // in global memory (L1/L2-resident, read once per hit).
         S.base = (__attribute__((address_space(3))) uint32_t*)reinterpret_cast<uint32_t*>(smem) + threadIdx.x;
-        double4* scene = smem + bvh_stack_bytes(p.stack_cap) / sizeof(double4);
+        S.lds = p.stack_lds;
+        S.stride = gridDim.x * blockDim.x;
+        if constexpr (kSpill) S.ovf = p.stack_ovf + blockIdx.x * blockDim.x + threadIdx.x;
+        double4* scene = smem + bvh_stack_bytes(p.stack_lds) / sizeof(double4);
         if constexpr (kLDS) {
             double4* lds_nodes = scene;
             double4* lds_geo = scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4));
@@ -944,13 +978,15 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
 
 using KernelFn = void (*)(KernelParams);
 
-static KernelFn pick_kernel(bool use_lds, bool bvh, bool stats) {
-    if (stats) {
-        if (use_lds) return bvh ? render_kernel<true, true, true> : render_kernel<true, false, true>;
-        return bvh ? render_kernel<false, true, true> : render_kernel<false, false, true>;
-    }
-    if (use_lds) return bvh ? render_kernel<true, true, false> : render_kernel<true, false, false>;
-    return bvh ? render_kernel<false, true, false> : render_kernel<false, false, false>;
+template <bool kBVH, bool kSpill>
+static KernelFn pick_kernel2(bool use_lds, bool stats) {
+    if (stats) return use_lds ? render_kernel<true, kBVH, true, kSpill> : render_kernel<false, kBVH, true, kSpill>;
+    return use_lds ? render_kernel<true, kBVH, false, kSpill> : render_kernel<false, kBVH, false, kSpill>;
+}
+
+static KernelFn pick_kernel(bool use_lds, bool bvh, bool stats, bool spill) {
+    if (!bvh) return pick_kernel2<false, false>(use_lds, stats);
+    return spill ? pick_kernel2<true, true>(use_lds, stats) : pick_kernel2<true, false>(use_lds, stats);
 }
 
 static KernelFn pick_resolve(int fmt) {
@@ -972,9 +1008,25 @@ static int resident_blocks(int device, KernelFn fn, int threads, size_t lds) {
     return cus * per_cu;
 }
 
+// Scene bytes staged in LDS (nodes, geometry, indices, leaf table), 16-B aligned.
+static size_t scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves) {
+    const size_t b = (size_t)n_nodes * sizeof(Bvh4Node) + (size_t)n_slots * (sizeof(double4) + sizeof(int32_t)) +
+                     (size_t)n_leaves * sizeof(int32_t);
+    return (b + 15) / 16 * 16;
+}
+
 size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap) {
-    return kUniformsBytes + bvh_stack_bytes(stack_cap) + (size_t)n_nodes * sizeof(Bvh4Node) +
-           (size_t)n_slots * (sizeof(double4) + sizeof(int32_t)) + (size_t)n_leaves * sizeof(int32_t);
+    return kUniformsBytes + bvh_stack_bytes(std::min(stack_cap, kStackLdsMin)) +
+           scene_lds_bytes(n_nodes, n_slots, n_leaves);
+}
+
+size_t bvh_stack_overflow_bytes(int32_t stack_cap, int device) {
+    if (stack_cap <= kStackLdsMin) return 0;
+    hipDeviceProp_t prop;
+    size_t lanes = (size_t)256 * 2048;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess)
+        lanes = (size_t)prop.multiProcessorCount * (size_t)prop.maxThreadsPerMultiProcessor;
+    return (size_t)(stack_cap - kStackLdsMin) * lanes * sizeof(uint32_t);
 }
 
 uint64_t max_band_samples() {
@@ -1014,10 +1066,16 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     bool use_lds;
     size_t lds;
     if (use_bvh) {
-        const size_t full = bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap);
-        use_lds = full <= kMaxLDSBytes;
-        lds = use_lds ? (full + 15) / 16 * 16 : kUniformsBytes + bvh_stack_bytes(p.stack_cap);
-        if (lds > kMaxLDSBytes) return hipErrorInvalidValue;  // stack bound checked when the scene is built
+        // Scene in LDS when it fits next to kStackLdsMin stack slots; the stack
+        // then takes what LDS is left (up to its bound), the rest spills.
+        const size_t scene = scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves);
+        use_lds = bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap) <= kMaxLDSBytes;
+        const size_t room = kMaxLDSBytes - kUniformsBytes - (use_lds ? scene : 0);
+        p.stack_lds = std::min<int32_t>(p.stack_cap, (int32_t)(room / kStackSlotBytes));
+        if (const char* cap = getenv("TRAY_STACK_LDS_SLOTS"))  // tests: force the overflow path
+            p.stack_lds = std::min(p.stack_lds, std::max<int32_t>(kStackLdsMin, atoi(cap)));
+        if (p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
+        lds = kUniformsBytes + bvh_stack_bytes(p.stack_lds) + (use_lds ? scene : 0);
     } else {
         const size_t geo = (size_t)p.n_pad * sizeof(double4);
         use_lds = geo + kUniformsBytes <= kMaxLDSBytes;
@@ -1025,7 +1083,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     }
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
-    const KernelFn fn = pick_kernel(use_lds, use_bvh, stats);
+    const KernelFn fn = pick_kernel(use_lds, use_bvh, stats, use_bvh && p.stack_cap > p.stack_lds);
     const KernelFn resolve = pick_resolve(p.out_format);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {

@@ -62,6 +62,8 @@ struct KernelParams {
     const MatRec* bmat;     // shading record per slot
     int32_t n_nodes, n_slots, n_leaves;
     int32_t stack_cap;      // traversal stack slots per lane (Bvh::stack_max + 1)
+    int32_t stack_lds;      // slots kept in LDS (set by launch_render)
+    uint32_t* stack_ovf;    // slots beyond the LDS ones, stride = grid lanes
     unsigned long long* stats;  // nullable: [segments, sphere tests, box tests]
     int32_t width, height, spp, max_depth;
     int32_t y_start, rows, tile_rows, tile_count, tile_index;
@@ -89,6 +91,9 @@ bool band_fits(int32_t width, int32_t spp);
 // LDS the BVH kernel needs to hold the whole BVH scene (plus its traversal
 // stacks) on chip; above kMaxLDSBytes it reads the scene from global memory.
 size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap);
+// Bytes of global stack-overflow area a render of a scene with this stack bound
+// needs on `device` (0 when the whole stack fits in LDS).
+size_t bvh_stack_overflow_bytes(int32_t stack_cap, int device);
 
 // Padded geometry length for n spheres (see KernelParams::geo).
 inline int32_t padded_spheres(int32_t n) { return ((n + 3) / 4) * 4 + 4; }
