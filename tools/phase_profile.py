@@ -41,12 +41,14 @@ def main():
     v = allv[:19]
     se = allv[32:]
     names = ["segments", "sphere_tests", "box_tests", "cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade",
-             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "unused_11", "unused_12", "rt_end_max", "rt_life_sum",
+             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "node_leafwait_lanes", "node_shadewait_lanes", "rt_end_max", "rt_life_sum",
              "rt_start_min_inv"]
     d = dict(zip(names, v))
     cyc = sum(d[k] for k in PHASES)
     d["share"] = {k: round(d[k] / cyc, 3) for k in PHASES}
     d["lanes_per_node_iter"] = round(d["node_lanes"] / max(1, d["node_iters"]), 1)
+    d["leafwait_lanes_per_node_iter"] = round(d["node_leafwait_lanes"] / max(1, d["node_iters"]), 1)
+    d["shadewait_lanes_per_node_iter"] = round(d["node_shadewait_lanes"] / max(1, d["node_iters"]), 1)
     d["lanes_per_leaf_phase"] = round(d["leaf_lanes"] / max(1, d["leaf_phases"]), 1)
     d["lanes_per_shade_phase"] = round(d["shade_lanes"] / max(1, d["shade_phases"]), 1)
     d["cyc_per_node_iter"] = round(d["cyc_node"] / max(1, d["node_iters"]), 1)

@@ -212,6 +212,14 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         m.radius = s.radius;
         m.rinv = 1.0 / s.radius;  // correctly rounded on the host
         m.pinv = 1.0 / s.param;
+        if (s.material == TRAY_DIELECTRIC) {  // Reflectance's r0 for both faces (same ops as the kernel)
+            for (int f = 0; f < 2; ++f) {
+                const double ref_idx = f == 0 ? m.pinv : s.param;
+                double r0 = (1 - ref_idx) / (1 + ref_idx);
+                r0 *= r0;
+                m.albedo[f] = r0;
+            }
+        }
         m.type = s.material;
         m.pad = 0;
     }

@@ -96,10 +96,9 @@ __device__ __forceinline__ D3 refract(D3 uv, D3 n, double eta) {
     const D3 par = smul(n, -__builtin_sqrt(__builtin_fabs(1.0 - length_sq(perp))));
     return add(perp, par);
 }
-// Reflectance (ray/materials.go:66-71); math.Pow(x,5) == x*((x*x)*(x*x)).
-__device__ __forceinline__ double reflectance(double cosine, double ref_idx) {
-    double r0 = (1 - ref_idx) / (1 + ref_idx);
-    r0 *= r0;
+// Reflectance (ray/materials.go:66-71) given r0 = ((1 - ref_idx) / (1 + ref_idx))^2,
+// precomputed per face on the host; math.Pow(x,5) == x*((x*x)*(x*x)).
+__device__ __forceinline__ double reflectance(double cosine, double r0) {
     const double x = 1 - cosine;
     const double x2 = x * x;
     const double x4 = x2 * x2;
@@ -144,12 +143,10 @@ constexpr size_t kUniformsBytes = (sizeof(Uniforms) + 255) / 256 * 256;
 __device__ __forceinline__ D3 ld3(const volatile __attribute__((address_space(3))) double* v) { return d3(v[0], v[1], v[2]); }
 
 // RandomUnitVector (ray/rand.go:30-32): Archimedes' projection of two uniforms of
-// the bounce's scatter block, z = 1 - 2 u0, phi = 2 pi u1.
-__device__ __forceinline__ D3 unit_vector_from(const U4& u) {
-    const double z = 1.0 - 2.0 * u.u0;
-    const double r = __builtin_sqrt(1.0 - z * z);
+// the bounce's scatter block, z = 1 - 2 u0, r = sqrt(1 - z*z), phi = 2 pi u1.
+__device__ __forceinline__ D3 unit_vector_from(double z, double r, double u1) {
     double s, c;
-    sincos_2pi(u.u1, s, c);
+    sincos_2pi(u1, s, c);
     return d3(r * c, r * s, z);
 }
 
@@ -654,9 +651,13 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         bool scattered = true;
         D3 new_dir;
         D3 att = d3(m.albedo[0], m.albedo[1], m.albedo[2]);
-        const bool lambertian = m.type == kLambertian;
+        const bool lambertian = m.type == kLambertian, dielectric = m.type == kDielectric;
+        // One sqrt serves RandomUnitVector's sqrt(1 - z^2) and Dielectric's sin_theta.
+        const double cos_theta = go_min(dot(neg(ud), normal), 1.0);
+        const double z = 1.0 - 2.0 * u.u0;
+        const double sq = __builtin_sqrt(dielectric ? 1.0 - cos_theta * cos_theta : 1.0 - z * z);
         D3 uv = d3(0, 0, 0);
-        if (lambertian || (m.type == kMetal && m.param > 0.0)) uv = unit_vector_from(u);
+        if (lambertian || (m.type == kMetal && m.param > 0.0)) uv = unit_vector_from(z, sq, u.u1);
         if (lambertian) {  // ray/materials.go:13-20
             new_dir = add(normal, uv);
             if (near_zero(new_dir)) new_dir = normal;
@@ -668,9 +669,9 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         } else {  // Dielectric, ray/materials.go:44-64
             att = d3(1.0, 1.0, 1.0);
             const double ratio = front ? m.pinv : m.param;  // 1.0/RefIdx precomputed (same bits)
-            const double cos_theta = go_min(dot(neg(ud), normal), 1.0);
-            const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
-            const bool do_reflect = ratio * sin_theta > 1.0 || reflectance(cos_theta, ratio) > u.u0;
+            const double sin_theta = sq;
+            const double r0 = front ? m.albedo[0] : m.albedo[1];
+            const bool do_reflect = ratio * sin_theta > 1.0 || reflectance(cos_theta, r0) > u.u0;
             new_dir = do_reflect ? reflect(ud, normal) : refract(ud, normal, ratio);
         }
         if (scattered) {
@@ -870,6 +871,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     if (m == 0ull) break;
                     PROF_CNT(4, 1);
                     PROF_CNT(5, __popcll(m));
+                    PROF_CNT(11, __popcll(__ballot(state == kLeafState)));   // waiting for the leaf phase
+                    PROF_CNT(12, __popcll(__ballot(state == kShadeState)));  // waiting for the shade phase
                     if (state == kTravState) {
                         uint32_t tested;
                         state = trav_node(T, sv, S, tested);

@@ -20,7 +20,8 @@ constexpr size_t kMaxLDSBytes = 160 * 1024;
 
 // Per-sphere shading record, read only for the closest hit (64 B).
 struct MatRec {
-    double albedo[3];
+    double albedo[3];  // Dielectric (attenuation 1): albedo[0], [1] hold Schlick's r0 for the
+                       // front (ratio 1/RefIdx) and back (ratio RefIdx) faces, ray/materials.go:67-68
     double param;   // Metal.Fuzz / Dielectric.RefIdx
     double radius;  // Sphere.Radius (normal = (P - C) / R, ray/objects.go:100)
     double rinv;    // RN(1 / Radius): exact quotients via div_rcp (tray_kernel.hip)
