@@ -12,20 +12,21 @@ ends with ONE RCCL gather of the row tiles to rank 0 ("scaling": "strong": the
 frame is fixed as N grows). value = W*H*r*steps / max-over-ranks wall time.
 
 Also reported (rank 0):
-  roofline     the megakernel against the VALU roof (it is compute bound; HBM
-               traffic is far below its roof and reported under "hbm"):
-               achieved = algorithmic VALU work per launch / mean launch time,
-               in lane-ops (every non-packed FP32/FP64 VALU op takes the same
-               issue slot; no FMA is allowed in the FP64 arithmetic, so the peak
-               is 78.6 TFLOP/s / 2 = 39.3 T ops/s). Work = 17 FP64 ops per
-               ray-sphere test + 60 per segment + 40 per sample
-               + 11 FP32 ops per ray-box test of the exact-culling BVH (6 FMA + 5
-               min/max/compare). Segments, sphere and box tests are counted by the
-               kernel itself in an untimed instrumented launch (segments are
-               bit-exact with the oracle). The timed launch is the megakernel plus
-               its per-pixel resolve pass (both kernels are on the stream between
-               the two HIP events); "brute_force_equiv" rates the same frame at the
-               reference's all-spheres-per-segment work.
+  roofline     the megakernel against the FP64 VALU roof (it is compute and
+               latency bound; HBM traffic is far below its roof and reported
+               under "hbm"): achieved = algorithmic VALU work per launch / mean
+               launch time, in FP64-op equivalents. No FMA is allowed in the FP64
+               arithmetic, so the peak is 78.6 TFLOP/s / 2 = 39.3 T ops/s (a
+               wave64 FP64 op issues in 4 cycles on a SIMD-32); an FP32 op issues
+               in 2 cycles (MI355X_MICROARCH.md) and counts 1/2. Work = 17 FP64
+               ops per ray-sphere test + 60 per segment + 40 per
+               sample + 11 FP32 ops per ray-box test of the exact-culling BVH (6
+               FMA + 5 min/max/compare). Segments, sphere and box tests are
+               counted by the kernel itself in an untimed instrumented launch
+               (segments are bit-exact with the oracle). The timed launch is the
+               megakernel plus its per-pixel resolve pass (both kernels are on the
+               stream between the two HIP events); "brute_force_equiv" rates the
+               same frame at the reference's all-spheres-per-segment work.
   cpu_baseline the oracle (C port of the reference's CPU loop with the
                reference's chunk-queue scheduler, ray/tracer.go:86-116) timed on
                a bounded row sample of the same frame on the host cores.
@@ -66,7 +67,7 @@ def main() -> int:
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--tile-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-row-step", type=int, default=2, help="oracle renders every k-th row of the frame")
+    ap.add_argument("--cpu-row-step", type=int, default=1, help="oracle renders every k-th row of the frame")
     ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")
     args = ap.parse_args()
 
@@ -165,7 +166,7 @@ def main() -> int:
         local_samples = rows * W * spp
         ops64 = 17.0 * sphere_tests + 60.0 * segments_local + 40.0 * local_samples
         ops32 = 11.0 * box_tests
-        ops = ops64 + ops32
+        ops = ops64 + 0.5 * ops32
         brute = 17.0 * len(spheres) * segments_local + 60.0 * segments_local + 40.0 * local_samples
         achieved = ops / (kernel_ms * 1e-3) / 1e12
         # megakernel: one 24-B colour per sample into the sample buffer + the scene
@@ -191,8 +192,9 @@ def main() -> int:
             "box_tests_per_launch": box_tests,
             "fp64_ops_per_launch": ops64,
             "fp32_ops_per_launch": ops32,
-            "ops_model": "VALU lane-ops: 17/sphere test + 60/segment + 40/sample (FP64, no FMA; SURVEY.md 8d) "
-                         "+ 11/box test (FP32); peak = 78.6 TFLOP/s FP64 vector spec / 2 = 39.3 T ops/s",
+            "ops_model": "FP64-op equivalents: 17/sphere test + 60/segment + 40/sample (FP64, no FMA; SURVEY.md 8d) "
+                         "+ 0.5 x 11/box test (FP32 issues at 2x FP64 on SIMD-32); "
+                         "peak = 78.6 TFLOP/s FP64 vector spec / 2 = 39.3 T ops/s",
             "brute_force_equiv": {"ops_per_launch": brute,
                                   "TFLOPs": round(brute / (kernel_ms * 1e-3) / 1e12, 3),
                                   "note": "reference work (every sphere tested per segment) / measured time"},
@@ -225,7 +227,7 @@ def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step):
     samples = len(rows) * W * spp
     return {"value": round(samples / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
             "seconds": round(dt, 3),
-            "sample": f"every {row_step}th row of the same frame ({len(rows)} rows x {W} px x r={spp}), "
+            "sample": f"every {row_step}. row of the same frame ({len(rows)} rows x {W} px x r={spp}), "
                       f"oracle/tray_oracle.c, {cores} pthreads"}
 
 

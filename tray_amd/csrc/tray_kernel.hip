@@ -323,19 +323,8 @@ __device__ __forceinline__ float f32_up(double v) {
 // Lane states of the BVH kernel.
 enum : uint32_t { kIdleState = 0, kTravState = 1, kLeafState = 2, kShadeState = 3 };
 
-// 1: slab distances of two children per packed FMA (v_pk_fma_f32).
-#ifndef TRAY_PK_FMA
-#define TRAY_PK_FMA 0
-#endif
-typedef float tray_f2 __attribute__((ext_vector_type(2)));
-typedef float tray_f4 __attribute__((ext_vector_type(4)));
-
 struct Trav {
-#if TRAY_PK_FMA
-    tray_f2 ixv, iyv, izv, oxv, oyv, ozv;  // FP32 ray, each value twice: t = box * inv - org * inv
-#else
     float ix, iy, iz, oix, oiy, oiz;  // FP32 ray: t = box * inv - org * inv
-#endif
     float tlim;                       // closest rounded up to float
     int32_t near_x, near_y, near_z;   // byte offsets of the near planes in a node
     uint32_t cur;                     // child reference to visit next (kBvhNone: done)
@@ -419,17 +408,8 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
     const float iy = __builtin_amdgcn_rcpf(dyf);
     const float iz = __builtin_amdgcn_rcpf(dzf);
     const float oix = (float)org.x * ix, oiy = (float)org.y * iy, oiz = (float)org.z * iz;
-#if TRAY_PK_FMA
-    T.ixv = tray_f2{ix, ix};
-    T.iyv = tray_f2{iy, iy};
-    T.izv = tray_f2{iz, iz};
-    T.oxv = tray_f2{-oix, -oix};
-    T.oyv = tray_f2{-oiy, -oiy};
-    T.ozv = tray_f2{-oiz, -oiz};
-#else
     T.ix = ix, T.iy = iy, T.iz = iz;
     T.oix = oix, T.oiy = oiy, T.oiz = oiz;
-#endif
     // Bvh4Node::box[a][s]: the near plane is the low one when the ray runs up the axis.
     T.near_x = ix < 0.0f ? 16 : 0;
     T.near_y = iy < 0.0f ? 48 : 32;
@@ -478,19 +458,6 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
     const uint4 rf = *reinterpret_cast<const uint4*>(nb + 96);
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for a pop
     const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
-#if TRAY_PK_FMA
-#define TRAY_PK(off, iv, ov, A, B)                                       \
-    const tray_f4 A##_v = *reinterpret_cast<const tray_f4*>(nb + (off)); \
-    const tray_f2 A = __builtin_elementwise_fma(A##_v.lo, iv, ov), B = __builtin_elementwise_fma(A##_v.hi, iv, ov);
-    TRAY_PK(T.near_x, T.ixv, T.oxv, tnx01, tnx23) TRAY_PK(T.near_x ^ 16, T.ixv, T.oxv, tfx01, tfx23)
-    TRAY_PK(T.near_y, T.iyv, T.oyv, tny01, tny23) TRAY_PK(T.near_y ^ 16, T.iyv, T.oyv, tfy01, tfy23)
-    TRAY_PK(T.near_z, T.izv, T.ozv, tnz01, tnz23) TRAY_PK(T.near_z ^ 16, T.izv, T.ozv, tfz01, tfz23)
-#undef TRAY_PK
-    (void)nx, (void)fx, (void)ny, (void)fy, (void)nz, (void)fz;
-    const float tnx[4] = {tnx01.x, tnx01.y, tnx23.x, tnx23.y}, tfx[4] = {tfx01.x, tfx01.y, tfx23.x, tfx23.y};
-    const float tny[4] = {tny01.x, tny01.y, tny23.x, tny23.y}, tfy[4] = {tfy01.x, tfy01.y, tfy23.x, tfy23.y};
-    const float tnz[4] = {tnz01.x, tnz01.y, tnz23.x, tnz23.y}, tfz[4] = {tfz01.x, tfz01.y, tfz23.x, tfz23.y};
-#else
     const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
     const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
     const float nza[4] = {nz.x, nz.y, nz.z, nz.w}, fza[4] = {fz.x, fz.y, fz.z, fz.w};
@@ -504,7 +471,6 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
         tnz[k] = __builtin_fmaf(nza[k], T.iz, -T.oiz);
         tfz[k] = __builtin_fmaf(fza[k], T.iz, -T.oiz);
     }
-#endif
     // An unused child's planes are (+inf, -inf): tn = +inf, never a hit.
     uint32_t key[4];
 #pragma unroll
