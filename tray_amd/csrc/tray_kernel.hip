@@ -574,10 +574,14 @@ __device__ __forceinline__ void start_sample(const KernelParams& p, UniPtr uni, 
 // ray/tracer.go:143), count its segments, free the lane.
 template <bool kStats>
 __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st) {
+#ifndef TRAY_DIAG_NO_STORE
     double* o = p.samples + (size_t)L.item * 3;
     o[0] = color.x;
     o[1] = color.y;
     o[2] = color.z;
+#else  // diagnostic only: measures what the sample stores cost (wrong images)
+    if (color.x == 12345.0) p.samples[0] = color.y;
+#endif
     if (p.segments) atomicAdd(p.segments + (size_t)L.j * (size_t)p.width + (size_t)L.x, L.segments);
     if constexpr (kStats) st.segments += L.segments;
     L.busy = false;
@@ -784,6 +788,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         PROF_T0();
         uint64_t idle = __ballot(!L.busy);
         if (__popcll(idle) < TRAY_REFILL_BATCH && idle != ~0ull) idle = 0ull;  // batch refills
+        // Items are assigned first (cheap, may span two chunks); the camera rays of
+        // all newly assigned lanes are then generated together.
+        uint32_t fresh_item = ~0u;
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
                 const uint32_t c = __shfl(next_chunk, 0);
@@ -797,24 +804,24 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             }
             const uint32_t n_idle = (uint32_t)__popcll(idle);
             const uint32_t take = min(n_idle, pool_end - pool_next);
-            if (!L.busy) {
+            if ((idle >> lane) & 1ull) {
                 const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
-                if (rank < take) {
-                    int32_t x, j;
-                    uint32_t smp;
-                    const uint32_t item = pool_next + rank;
-                    if (item < p.items && decode_item(p, item, x, j, smp)) {
-                        start_sample(p, uni, L, item, x, j, smp);
-                        if constexpr (kBVH) {
-                            ++L.segments;
-                            trav_begin(T, L.org, L.dir);
-                            state = sv.n_nodes > 0 ? kTravState : kShadeState;
-                        }
-                    }
-                }
+                if (rank < take) fresh_item = pool_next + rank;
             }
             pool_next += take;
-            idle = __ballot(!L.busy);
+            idle = __ballot(!L.busy && fresh_item == ~0u);
+        }
+        if (fresh_item != ~0u) {
+            int32_t x, j;
+            uint32_t smp;
+            if (fresh_item < p.items && decode_item(p, fresh_item, x, j, smp)) {
+                start_sample(p, uni, L, fresh_item, x, j, smp);
+                if constexpr (kBVH) {
+                    ++L.segments;
+                    trav_begin(T, L.org, L.dir);
+                    state = sv.n_nodes > 0 ? kTravState : kShadeState;
+                }
+            }
         }
         PROF_ADD(0);
         if (__ballot(L.busy) == 0ull) break;
