@@ -824,7 +824,10 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             }
         }
         PROF_ADD(0);
-        if (__ballot(L.busy) == 0ull) break;
+        if (__ballot(L.busy) == 0ull) {
+            if (exhausted) break;  // (a prefetched chunk must not be dropped)
+            continue;              // every lane drew a padding item: draw again
+        }
 
         if constexpr (!kBVH) {
             if (L.busy) {
