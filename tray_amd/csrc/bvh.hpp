@@ -37,7 +37,7 @@ static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
 
 struct Bvh {
     std::vector<Bvh4Node> nodes;  // nodes[0] is the root (always an inner node)
-    std::vector<int32_t> leaves;  // per leaf: (first slot << 3) | sphere count
+    std::vector<int32_t> leaves;  // per leaf: (first slot << 3) | sphere count (leaf_max 1: slot == leaf index)
     std::vector<double4> geo;     // {cx, cy, cz, R*R} in leaf-slot order
     std::vector<int32_t> idx;     // original list index of each slot
     double bound = 0;             // M: every box coordinate lies in [-M, M]

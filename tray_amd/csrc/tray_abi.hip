@@ -392,6 +392,7 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.n_slots = sc->n_slots;
     k.n_leaves = sc->n_leaves;
     k.leaves = sc->leaves;
+    k.leaf_single = sc->leaf_max == 1 ? 1 : 0;
     k.stack_ovf = sc->stack_ovf;
     k.stack_cap = sc->stack_cap;
     // The BVH's conservative FP32 box test assumes every ray origin lies within

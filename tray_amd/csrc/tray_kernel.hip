@@ -273,6 +273,7 @@ struct SceneView {
     const double4* geo;     // linear scan: list order, NaN-padded
     const Bvh4Node* nodes;  // BVH: 4-wide nodes, root first
     const int32_t* leaves;  // BVH: per leaf (first slot << 3) | count
+    bool single;            // BVH: one sphere per leaf, leaf index == slot
     const double4* bgeo;    // BVH: spheres in leaf-slot order
     const int32_t* bidx;    // BVH: original list index of each slot
     const MatRec* bmat;     // BVH: shading record of each slot
@@ -505,7 +506,9 @@ template <class Stk>
 __device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const Stk& S, const D3& org,
                                               const D3& dir, uint32_t& tested) {
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for the pop
-    const int32_t info = sv.leaves[T.cur & (kBvhLeafBit - 1u)];
+    // One sphere per leaf: the leaf index is its slot (no leaf-table round trip).
+    const int32_t info = sv.single ? (int32_t)(((T.cur & (kBvhLeafBit - 1u)) << 3) | 1u)
+                                   : sv.leaves[T.cur & (kBvhLeafBit - 1u)];
     const int32_t first = info >> 3, end = first + (info & 7);
     tested = 0;
     for (int32_t slot = first; slot < end; ++slot) {
@@ -732,7 +735,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         u->seed = p.seed;
     }
     const UniPtr uni = uni_lds;
-    SceneView sv{p.geo, p.nodes, p.leaves, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
+    SceneView sv{p.geo, p.nodes, p.leaves, p.leaf_single != 0, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
     Stack<kSpill> S{nullptr, nullptr, 0, 0};
     if constexpr (kBVH) {
         // [stacks: stack_cap x blockDim x 4 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]

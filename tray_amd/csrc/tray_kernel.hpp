@@ -58,6 +58,7 @@ struct KernelParams {
     double* samples;     // per-item path colours (3 doubles), summed in order by the resolve kernel
     const Bvh4Node* nodes;  // exact-culling 4-wide BVH (tray_bvh.cpp), root first
     const int32_t* leaves;  // per leaf: (first slot << 3) | count
+    int32_t leaf_single;    // 1: every leaf holds one sphere and its index is its slot
     const double4* bgeo;    // spheres in leaf-slot order
     const int32_t* bidx;    // original index per slot
     const MatRec* bmat;     // shading record per slot
