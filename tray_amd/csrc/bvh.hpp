@@ -10,7 +10,11 @@
 
 namespace tray {
 
-constexpr int kBvhWidth = 4;
+#ifndef TRAY_BVH_WIDTH
+#define TRAY_BVH_WIDTH 4
+#endif
+constexpr int kBvhWidth = TRAY_BVH_WIDTH;  // children per node: 4 or 8
+static_assert(kBvhWidth == 4 || kBvhWidth == 8, "BVH width");
 // Spheres per leaf: 1 by default (every sphere gets its own padded box, which
 // is then the FP32 pre-test of its FP64 intersection); up to 4 when the node
 // count must shrink.
@@ -31,9 +35,9 @@ constexpr int32_t kBvhMaxLeaves = 0x7FFF;
 struct Bvh4Node {
     float box[3][2][kBvhWidth];  // [axis][lo, hi][child]
     uint32_t ref[kBvhWidth];     // 16-bit child references (above)
-    uint32_t pad[4];
+    uint32_t pad[kBvhWidth == 4 ? 4 : 0];
 };
-static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
+static_assert(sizeof(Bvh4Node) % 32 == 0, "Bvh4Node layout");
 
 struct Bvh {
     std::vector<Bvh4Node> nodes;  // nodes[0] is the root (always an inner node)

@@ -412,9 +412,10 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
     T.ix = ix, T.iy = iy, T.iz = iz;
     T.oix = oix, T.oiy = oiy, T.oiz = oiz;
     // Bvh4Node::box[a][s]: the near plane is the low one when the ray runs up the axis.
-    T.near_x = ix < 0.0f ? 16 : 0;
-    T.near_y = iy < 0.0f ? 48 : 32;
-    T.near_z = iz < 0.0f ? 80 : 64;
+    constexpr int32_t kPlane = 4 * kBvhWidth;  // bytes of one plane block (one float per child)
+    T.near_x = ix < 0.0f ? kPlane : 0;
+    T.near_y = 2 * kPlane + (iy < 0.0f ? kPlane : 0);
+    T.near_z = 4 * kPlane + (iz < 0.0f ? kPlane : 0);
 }
 
 // Push `key` if valid. The store is unconditional: with no push it writes
@@ -448,52 +449,58 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t be
 // Returns the new lane state.
 template <class Stk>
 __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, const Stk& S, uint32_t& tested) {
+    constexpr int32_t kPlane = 4 * kBvhWidth;  // far plane block = near ^ kPlane
     const char* nb = reinterpret_cast<const char*>(sv.nodes + T.cur);
-    // Near and far planes of the four children on each axis (far = near ^ 16).
-    const float4 nx = *reinterpret_cast<const float4*>(nb + T.near_x);
-    const float4 fx = *reinterpret_cast<const float4*>(nb + (T.near_x ^ 16));
-    const float4 ny = *reinterpret_cast<const float4*>(nb + T.near_y);
-    const float4 fy = *reinterpret_cast<const float4*>(nb + (T.near_y ^ 16));
-    const float4 nz = *reinterpret_cast<const float4*>(nb + T.near_z);
-    const float4 fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ 16));
-    const uint4 rf = *reinterpret_cast<const uint4*>(nb + 96);
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for a pop
-    const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
-    const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
-    const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
-    const float nza[4] = {nz.x, nz.y, nz.z, nz.w}, fza[4] = {fz.x, fz.y, fz.z, fz.w};
-    float tnx[4], tfx[4], tny[4], tfy[4], tnz[4], tfz[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {  // slab distances: t = plane * inv - org * inv
-        tnx[k] = __builtin_fmaf(nxa[k], T.ix, -T.oix);
-        tfx[k] = __builtin_fmaf(fxa[k], T.ix, -T.oix);
-        tny[k] = __builtin_fmaf(nya[k], T.iy, -T.oiy);
-        tfy[k] = __builtin_fmaf(fya[k], T.iy, -T.oiy);
-        tnz[k] = __builtin_fmaf(nza[k], T.iz, -T.oiz);
-        tfz[k] = __builtin_fmaf(fza[k], T.iz, -T.oiz);
-    }
+    // Hit children: upper 16 bits of the entry distance | reference (tn >= 0, so
+    // the keys order like the distances, to bf16 precision); anything else ~0.
     // An unused child's planes are (+inf, -inf): tn = +inf, never a hit.
-    uint32_t key[4];
+    uint32_t key[kBvhWidth];
+    tested = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx[k], tny[k]), tnz[k]), 0.0f);
-        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fminf(tfx[k], tfy[k]), tfz[k]), T.tlim);
-        key[k] = tn <= tf ? ((__float_as_uint(tn) & 0xFFFF0000u) | ref[k]) : ~0u;
+    for (int g = 0; g < kBvhWidth / 4; ++g) {  // four children per group of 16-B loads
+        const float4 nx = *reinterpret_cast<const float4*>(nb + T.near_x + 16 * g);
+        const float4 fx = *reinterpret_cast<const float4*>(nb + (T.near_x ^ kPlane) + 16 * g);
+        const float4 ny = *reinterpret_cast<const float4*>(nb + T.near_y + 16 * g);
+        const float4 fy = *reinterpret_cast<const float4*>(nb + (T.near_y ^ kPlane) + 16 * g);
+        const float4 nz = *reinterpret_cast<const float4*>(nb + T.near_z + 16 * g);
+        const float4 fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ kPlane) + 16 * g);
+        const uint4 rf = *reinterpret_cast<const uint4*>(nb + 6 * kPlane + 16 * g);
+        const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
+        const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
+        const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
+        const float nza[4] = {nz.x, nz.y, nz.z, nz.w}, fza[4] = {fz.x, fz.y, fz.z, fz.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // slab distances: t = plane * inv - org * inv
+            const float tnx = __builtin_fmaf(nxa[k], T.ix, -T.oix), tfx = __builtin_fmaf(fxa[k], T.ix, -T.oix);
+            const float tny = __builtin_fmaf(nya[k], T.iy, -T.oiy), tfy = __builtin_fmaf(fya[k], T.iy, -T.oiy);
+            const float tnz = __builtin_fmaf(nza[k], T.iz, -T.oiz), tfz = __builtin_fmaf(fza[k], T.iz, -T.oiz);
+            const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz), 0.0f);
+            const float tf = __builtin_fminf(__builtin_fminf(__builtin_fminf(tfx, tfy), tfz), T.tlim);
+            key[4 * g + k] = tn <= tf ? ((__float_as_uint(tn) & 0xFFFF0000u) | ref[k]) : ~0u;
+            tested += ref[k] != kBvhNone ? 1u : 0u;
+        }
     }
-    tested = (uint32_t)(ref[0] != kBvhNone) + (uint32_t)(ref[1] != kBvhNone) + (uint32_t)(ref[2] != kBvhNone) +
-             (uint32_t)(ref[3] != kBvhNone);
 #define TRAY_CX(i, j)                             \
     {                                             \
         const uint32_t lo_ = min(key[i], key[j]); \
         key[j] = max(key[i], key[j]);             \
         key[i] = lo_;                             \
     }
-    TRAY_CX(0, 1) TRAY_CX(2, 3) TRAY_CX(0, 2) TRAY_CX(1, 3) TRAY_CX(1, 2)
+    if constexpr (kBvhWidth == 4) {
+        TRAY_CX(0, 1) TRAY_CX(2, 3) TRAY_CX(0, 2) TRAY_CX(1, 3) TRAY_CX(1, 2)
+    } else {  // 19-exchange network for 8
+        TRAY_CX(0, 2) TRAY_CX(1, 3) TRAY_CX(4, 6) TRAY_CX(5, 7)
+        TRAY_CX(0, 4) TRAY_CX(1, 5) TRAY_CX(2, 6) TRAY_CX(3, 7)
+        TRAY_CX(0, 1) TRAY_CX(2, 3) TRAY_CX(4, 5) TRAY_CX(6, 7)
+        TRAY_CX(2, 4) TRAY_CX(3, 5)
+        TRAY_CX(1, 4) TRAY_CX(3, 6)
+        TRAY_CX(1, 2) TRAY_CX(3, 4) TRAY_CX(5, 6)
+    }
 #undef TRAY_CX
     if (key[0] != ~0u) {
-        stack_push(T, S, key[3]);
-        stack_push(T, S, key[2]);
-        stack_push(T, S, key[1]);
+#pragma unroll
+        for (int k = kBvhWidth - 1; k >= 1; --k) stack_push(T, S, key[k]);
         T.cur = key[0] & 0xFFFFu;
     } else {
         T.cur = stack_pop(T, S, below);
