@@ -7,7 +7,8 @@ headline workload (config 2: book-cover scene, seed 2, 1280x720, r=64, d=50).
 
 A step = one full frame rendered through the C-ABI (tray_render_async) with the
 scene already resident in HBM; for N > 1 the frame is split into interleaved
-8-row tiles (one shard per rank, no collective inside the render) and the step
+row tiles (default 1 row: rank k renders rows y = k mod N; one shard per rank,
+no collective inside the render) and the step
 ends with ONE RCCL gather of the row tiles to rank 0 ("scaling": "strong": the
 frame is fixed as N grows). value = W*H*r*steps / max-over-ranks wall time.
 
@@ -65,7 +66,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--tile-rows", type=int, default=8)
+    ap.add_argument("--tile-rows", type=int, default=1, help="rows per interleaved tile (N > 1): 1 balances best")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-step", type=int, default=1, help="oracle renders every k-th row of the frame")
     ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")

@@ -11,7 +11,7 @@ import torch.multiprocessing as mp
 
 from conftest import DEFAULT_BG, RICH_SETUP
 
-W, H, SPP, DEPTH, SEED, TILE = 40, 29, 2, 12, 3, 4
+W, H, SPP, DEPTH, SEED = 40, 29, 2, 12, 3
 
 
 def _free_port():
@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, result_path):
+def _worker(rank, world, port, result_path, tile):
     import torch
     import torch.distributed as dist
 
@@ -30,9 +30,9 @@ def _worker(rank, world, port, result_path):
     from tray_amd import shard
 
     _, cam = O.camera_initialize(RICH_SETUP, W, H)
-    rows = shard.rows_for(H, TILE, world, rank)
+    rows = shard.rows_for(H, tile, world, rank)
     local = O.render_rows(O.rich_scene(2), DEFAULT_BG, cam, W, H, SPP, DEPTH, 0.5, SEED, rows, segments=False)
-    full = shard.gather_image(torch.from_numpy(local), H, TILE, world, rank)
+    full = shard.gather_image(torch.from_numpy(local), H, tile, world, rank)
     if rank == 0:
         np.save(result_path, full.numpy())
     else:
@@ -40,10 +40,10 @@ def _worker(rank, world, port, result_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gather_row_tiles_gloo(O, tmp_path, world):
+@pytest.mark.parametrize("world,tile", [(2, 4), (3, 4), (2, 1)])
+def test_gather_row_tiles_gloo(O, tmp_path, world, tile):
     path = str(tmp_path / "img.npy")
-    mp.spawn(_worker, args=(world, _free_port(), path), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), path, tile), nprocs=world, join=True)
     got = np.load(path)
     _, cam = O.camera_initialize(RICH_SETUP, W, H)
     ref = O.render(O.rich_scene(2), DEFAULT_BG, cam, W, H, SPP, DEPTH, 0.5, SEED, segments=False)
