@@ -2,7 +2,7 @@
 """Benchmark: Mrays/s of the MI355X path-tracing megakernel on BASELINE.json's
 headline workload (config 2: book-cover scene, seed 2, 1280x720, r=64, d=50).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 A step = one full frame rendered through the C-ABI (tray_render_async) with the
@@ -52,6 +52,7 @@ CONFIGS = {
     "c1": ("C1 book-cover seed 2 400x225 r=16 d=12", 2, 11, 400, 225, 16, 12),
     "c2": ("C2 book-cover seed 2 1280x720 r=64 d=50", 2, 11, 1280, 720, 64, 50),
     "c3": ("C3 book-cover seed 2 3840x2160 r=256 d=50", 2, 11, 3840, 2160, 256, 50),
+    "c4": ("C4 book-cover seed 2 3840x2160 r=1024 d=50 (8-GPU row tiles)", 2, 11, 3840, 2160, 1024, 50),
     "c5": ("C5 dense RichScene(half-extent 22) seed 7 1920x1080 r=256 d=50", 7, 22, 1920, 1080, 256, 50),
 }
 
@@ -152,7 +153,8 @@ def main() -> int:
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "strong",
-        "vs_baseline": None,
+        "vs_baseline": None,  # BASELINE.json "published" is empty
+        "reference_readme_mrays": 0.33,  # derived from README.md:30-31 (M3 Pro, 11 cores, C2, ~3 min); context only
         "dtype": "f64",
         "data": "synthetic: RichScene book-cover generator on the counter RNG (include/tray.h), RichSceneCamera",
         "config": {
