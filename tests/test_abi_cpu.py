@@ -174,3 +174,16 @@ def test_scene_info_layout(L):
     import ctypes
 
     assert ctypes.sizeof(L.SceneInfo) == 8 * 4 + 8
+
+
+def test_png_sink_round_trip():
+    """PNG sink (benchmark/benchmark.go:23-33 encodes Render's *image.RGBA)."""
+    import numpy as np
+
+    from tray_amd import png
+
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (17, 23, 4), dtype=np.uint8)
+    data = png.encode_png(img)
+    assert data[:8] == b"\x89PNG\r\n\x1a\n" and data[12:16] == b"IHDR"
+    assert np.array_equal(png.decode_png(data), img)

@@ -99,3 +99,15 @@ def test_seed_reproducible_and_sensitive(ray):  # Seed semantics (tracer.go:33)
 
     a, b, c = render(5), render(5), render(6)
     assert np.array_equal(a, b) and not np.array_equal(a, c)
+
+
+def test_render_to_png(ray, tmp_path):  # benchmark/benchmark.go:23-33: png.Encode(Render(scene))
+    from tray_amd import png
+
+    t = ray.New(32, 18)
+    t.Seed, t.NumRaysPerPixel, t.MaxDepth = 2, 4, 20
+    t.Camera = ray.RichSceneCamera()
+    img = t.Render(ray.RichScene(2))
+    path = str(tmp_path / "out.png")
+    png.save_png(path, img)
+    assert np.array_equal(png.decode_png(open(path, "rb").read()), img)
