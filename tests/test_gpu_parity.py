@@ -237,6 +237,29 @@ def test_bvh_adversarial_spheres(L, O):
     check(bvh, sb, ref, rseg)
 
 
+def test_bvh_global_spheres(L, O):
+    """Spheres kept out of the tree (tested first by every traversal): an enclosing
+    dome the camera sits inside, listed last, and the ground, listed first."""
+    from oracle.oracle import SPHERE_DTYPE
+
+    base = O.rich_scene(3)
+    s = np.zeros(len(base) + 1, dtype=SPHERE_DTYPE)
+    s[:len(base)] = base
+    s[-1]["center"], s[-1]["radius"], s[-1]["material"] = (0, 0, 0), 5000.0, 1  # dome (hit from inside)
+    s[-1]["albedo"] = (0.9, 0.8, 0.7)
+    dev = L.DeviceScene(s, bg_struct(L, DEFAULT_BG), 0)
+    i = dev.info()
+    dev.release()
+    assert i.has_bvh == 1 and i.n_global == 2 and i.bound == 5000.0
+    for setup, seed in ((RICH_SETUP, 3), (np.array([0.5, 30, 0.25, 0, 0, 0, 0, 0, 1, 40.0, 10.0, 30.0, 0.0]), 4)):
+        st = camera(L, setup, 64, 40)
+        bvh, sb = gpu_render(L, s, DEFAULT_BG, st, 64, 40, 4, 30, 0.5, seed)
+        lin, sl = gpu_render(L, s, DEFAULT_BG, st, 64, 40, 4, 30, 0.5, seed, flags=L.FLAG_LINEAR_SCAN)
+        assert np.array_equal(sb, sl) and np.array_equal(bvh, lin)
+    ref, rseg = O.render(s, DEFAULT_BG, st.as_array(), 64, 40, 4, 30, 0.5, seed, workers=WORKERS)
+    check(bvh, sb, ref, rseg)
+
+
 def test_stats_counters(L, O):
     import torch
 
@@ -268,7 +291,8 @@ def test_scene_info_and_traversal_paths(L, O):
     book = L.DeviceScene(O.rich_scene(2), bg_struct(L, DEFAULT_BG), 0)
     i = book.info()
     assert (i.n_spheres, i.has_bvh, i.leaf_max, i.lds_resident) == (486, 1, 1, 1)
-    assert 0 < i.stack_depth <= 48 and i.n_leaves == 486 and i.bound == 2000.0  # ground: y in [-2000, 0]
+    assert 0 < i.stack_depth <= 48 and i.bound == 2000.0  # ground: y in [-2000, 0]
+    assert i.n_global == 1 and i.n_leaves == 485  # the ground sphere is tested before the tree
     big = O.rich_scene(5, 40)
     ib = L.DeviceScene(big, bg_struct(L, DEFAULT_BG), 0).info()
     assert ib.has_bvh == 1 and ib.lds_resident == 0

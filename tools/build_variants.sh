@@ -3,7 +3,7 @@
 #   tools/build_variants.sh NAME "EXTRA HIPFLAGS" [NAME "FLAGS" ...]
 set -e
 cd "$(dirname "$0")/../tray_amd"
-BASE="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fvisibility=hidden"
+BASE="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -mllvm -amdgpu-atomic-optimizer-strategy=None -fvisibility=hidden"
 while [ $# -ge 2 ]; do
   NAME=$1; FLAGS=$2; shift 2
   OUT=build/variants/$NAME; mkdir -p $OUT

@@ -104,7 +104,7 @@ class SceneInfo(ctypes.Structure):
     """tray_scene_info: how an uploaded scene is traversed."""
     _fields_ = [("n_spheres", ctypes.c_int32), ("has_bvh", ctypes.c_int32), ("leaf_max", ctypes.c_int32),
                 ("n_nodes", ctypes.c_int32), ("n_leaves", ctypes.c_int32), ("stack_depth", ctypes.c_int32),
-                ("lds_resident", ctypes.c_int32), ("reserved", ctypes.c_int32), ("bound", ctypes.c_double)]
+                ("lds_resident", ctypes.c_int32), ("n_global", ctypes.c_int32), ("bound", ctypes.c_double)]
 
 
 class TrayError(RuntimeError):

@@ -27,6 +27,12 @@ constexpr uint32_t kBvhLeafBit = 0x8000u;
 constexpr uint32_t kBvhNone = 0xFFFFu;
 constexpr int32_t kBvhMaxNodes = 0x8000;
 constexpr int32_t kBvhMaxLeaves = 0x7FFF;
+// A sphere whose box dwarfs the rest of the scene (a ground sphere) is not put
+// in the tree: every traversal tests it first (nearly every ray would visit
+// it anyway), which also seeds the culling distance. At most kBvhGlobals, each
+// with a box surface kBvhGlobalRatio times that of all the other spheres.
+constexpr int kBvhGlobals = 2;
+constexpr double kBvhGlobalRatio = 16.0;
 
 // 128 B: the boxes of up to four children, SoA by axis so one node is seven
 // 16-byte LDS reads; box[a][0] / box[a][1] are the low / high planes on axis a
@@ -47,6 +53,7 @@ struct Bvh {
     double bound = 0;             // M: every box coordinate lies in [-M, M]
     int32_t stack_max = 0;        // deepest stack the ordered traversal can build
     int leaf_max = 1;
+    int32_t n_global = 0;         // spheres tested before the tree: the last n_global slots
 };
 
 // Returns false on non-finite input or a tree the kernel cannot index (the

@@ -102,7 +102,7 @@ struct tray_scene_s {
     // exact-culling BVH (absent for tiny or non-finite scenes)
     bool has_bvh;
     double bvh_bound;
-    int32_t n_nodes, n_slots, n_leaves, stack_cap, leaf_max;
+    int32_t n_nodes, n_slots, n_leaves, stack_cap, leaf_max, n_global;
     tray::Bvh4Node* nodes;
     int32_t* leaves;
     uint32_t* stack_ovf;  // traversal-stack slots beyond LDS (deep BVHs only)
@@ -253,6 +253,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->stack_ovf = nullptr;
     sc->stack_cap = bvh.stack_max + 1;
     sc->leaf_max = has_bvh ? bvh.leaf_max : 0;
+    sc->n_global = has_bvh ? bvh.n_global : 0;
     sc->nodes = nullptr;
     sc->bgeo = nullptr;
     sc->bidx = nullptr;
@@ -326,6 +327,7 @@ int tray_scene_get_info(tray_scene_t sc, tray_scene_info* out) {
                                            kMaxLDSBytes
                             ? 1
                             : 0;
+    out->n_global = sc->n_global;
     out->bound = sc->bvh_bound;
     return TRAY_OK;
 }
@@ -391,6 +393,7 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.n_nodes = sc->n_nodes;
     k.n_slots = sc->n_slots;
     k.n_leaves = sc->n_leaves;
+    k.n_global = sc->n_global;
     k.leaves = sc->leaves;
     k.leaf_single = sc->leaf_max == 1 ? 1 : 0;
     k.stack_ovf = sc->stack_ovf;

@@ -19,7 +19,10 @@
 //
 // Build: binned SAH over sphere centroids into a binary tree (object-median
 // splits once a branch gets deep, so depth stays bounded), then collapsed into
-// 4-wide nodes by repeatedly opening the largest-area inner child.
+// 4-wide nodes by repeatedly opening the largest-area inner child. Spheres
+// whose boxes dwarf the rest (kBvhGlobals) stay out of the tree and are tested
+// at the start of every traversal: visiting them first is one more any-order
+// visit, so the result is unchanged.
 
 #include <math.h>
 #include <stdint.h>
@@ -248,6 +251,7 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     out->idx.clear();
     out->bound = 0;
     out->stack_max = 0;
+    out->n_global = 0;
     if (n <= 0) return true;
     Builder B;
     B.prims.resize((size_t)n);
@@ -267,10 +271,29 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     m = std::max(m, 1.0);
     B.pad = 4e-6 * m;
     B.leaf_max = std::min(std::max(leaf_max, 1), kBvhLeafMax);
-    if (n <= B.leaf_max) return false;  // root must be an inner node
-    B.bin.reserve((size_t)2 * n);
-    const int root = B.build2(0, n, 0);
+    std::vector<Prim> globals;
+    while ((int)globals.size() < kBvhGlobals && (int)B.prims.size() > B.leaf_max + 1) {
+        size_t big = 0;
+        for (size_t i = 1; i < B.prims.size(); ++i)
+            if (B.prims[i].box.area() > B.prims[big].box.area()) big = i;
+        Box rest;
+        for (size_t i = 0; i < B.prims.size(); ++i)
+            if (i != big) rest.grow(B.prims[i].box);
+        if (!(B.prims[big].box.area() >= kBvhGlobalRatio * rest.area())) break;
+        globals.push_back(B.prims[big]);
+        B.prims.erase(B.prims.begin() + (std::ptrdiff_t)big);
+    }
+    const int32_t nt = (int32_t)B.prims.size();
+    if (nt <= B.leaf_max) return false;  // root must be an inner node
+    B.bin.reserve((size_t)2 * nt);
+    const int root = B.build2(0, nt, 0);
     B.collapse(root, 0, s);
+    std::sort(globals.begin(), globals.end(), [](const Prim& x, const Prim& y) { return x.index < y.index; });
+    for (const Prim& g : globals) {  // the last slots, after every leaf's
+        const tray_sphere& sp = s[g.index];
+        B.geo.push_back(make_double4(sp.center[0], sp.center[1], sp.center[2], sp.radius * sp.radius));
+        B.idx.push_back(g.index);
+    }
     if ((int64_t)B.nodes.size() > kBvhMaxNodes || (int64_t)B.leaves.size() > kBvhMaxLeaves) return false;
     out->nodes.swap(B.nodes);
     out->leaves.swap(B.leaves);
@@ -279,6 +302,7 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     out->bound = m;
     out->stack_max = B.stack_max;
     out->leaf_max = B.leaf_max;
+    out->n_global = (int32_t)globals.size();
     return true;
 }
 

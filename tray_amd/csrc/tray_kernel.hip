@@ -58,17 +58,27 @@ __device__ __forceinline__ D3 neg(D3 v) { return d3(-v.x, -v.y, -v.z); }
 // §4.7). 3 FP64 instructions instead of ~10 for the generic sequence; checked
 // on 10^9 pairs by tools/div_check.hip. Zero keeps its sign, and quotients near
 // the overflow/underflow range (or non-finite operands) take the full division.
-__device__ __forceinline__ double div_rcp(double a, double b, double y) {
+// Branch-free form: `ok` is cleared when the quotient needs the full division
+// (the caller then redoes its divisions in one rarely taken branch).
+__device__ __forceinline__ double div_rcp_try(double a, double b, double y, bool& ok) {
     const double q = a * y;
     const double r = __builtin_fma(-b, q, a);
     const double q1 = __builtin_fma(r, y, q);
     const double aq = __builtin_fabs(q);
-    if (a == 0) return q;
-    if (!(aq > 0x1p-960 && aq < 0x1p+960)) return a / b;
-    return q1;
+    ok = ok && (a == 0 || (aq > 0x1p-960 && aq < 0x1p+960));
+    return a == 0 ? q : q1;
+}
+__device__ __forceinline__ double div_rcp(double a, double b, double y) {
+    bool ok = true;
+    const double q = div_rcp_try(a, b, y, ok);
+    if (__builtin_expect(!ok, 0)) return a / b;
+    return q;
 }
 __device__ __forceinline__ D3 sdiv_rcp(D3 v, double t, double y) {
-    return d3(div_rcp(v.x, t, y), div_rcp(v.y, t, y), div_rcp(v.z, t, y));
+    bool ok = true;
+    const D3 q = d3(div_rcp_try(v.x, t, y, ok), div_rcp_try(v.y, t, y, ok), div_rcp_try(v.z, t, y, ok));
+    if (__builtin_expect(!ok, 0)) return sdiv(v, t);
+    return q;
 }
 __device__ __forceinline__ double dot(D3 u, D3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
 __device__ __forceinline__ double length_sq(D3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
@@ -278,6 +288,7 @@ struct SceneView {
     const int32_t* bidx;    // BVH: original list index of each slot
     const MatRec* bmat;     // BVH: shading record of each slot
     int32_t n, n_nodes;
+    int32_t n_global, global_first;  // BVH: spheres tested before the tree, their first slot
 };
 
 // Scene.Hit (ray/objects.go:37-46) as the reference's linear scan over
@@ -390,7 +401,7 @@ __device__ __forceinline__ uint32_t state_of(uint32_t ref) {
     return ref == kBvhNone ? kShadeState : (ref & kBvhLeafBit) ? kLeafState : kTravState;
 }
 
-__device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir) {
+__device__ __forceinline__ void trav_begin(Trav& T, const SceneView& sv, const D3& org, const D3& dir) {
     T.a = length_sq(dir);  // hoisted: same bits as per sphere
     T.a_inv = 1.0 / T.a;
     T.closest = __builtin_inf();
@@ -416,6 +427,19 @@ __device__ __forceinline__ void trav_begin(Trav& T, const D3& org, const D3& dir
     T.near_x = ix < 0.0f ? kPlane : 0;
     T.near_y = 2 * kPlane + (iy < 0.0f ? kPlane : 0);
     T.near_z = 4 * kPlane + (iz < 0.0f ? kPlane : 0);
+    // The spheres kept out of the tree (tray_bvh.cpp) are visited first; a hit
+    // seeds the culling distance of the whole traversal.
+    for (int32_t g = 0; g < sv.n_global; ++g) {
+        const int32_t slot = sv.global_first + g;
+        double h, d;
+        quad(sv.bgeo[slot], org, dir, T.a, h, d);
+        if (d >= 0) {
+            const int32_t before = T.best;
+            candidate_any_order(h, d, T.a, T.a_inv, sv.bidx[slot], T.closest, T.best);
+            if (T.best != before) T.slot = slot;
+        }
+    }
+    T.tlim = f32_up(T.closest);
 }
 
 // Push `key` if valid. The store is unconditional: with no push it writes
@@ -428,19 +452,25 @@ __device__ __forceinline__ void stack_push(Trav& T, const Stk& S, uint32_t key) 
     T.sp += valid ? 1 : 0;
 }
 
-// Pop entries until one whose box may still hold a closer hit (key_tn <= tlim:
-// the test of the box against the current closest hit, as at push time); its
-// reference, or kBvhNone. `below` = slot sp - 1, read ahead.
+// Pop the next entry to visit: the top, or (when the top's box lies beyond the
+// current closest hit, key_tn > tlim) the entry below it, read ahead in `below`.
+// One cull at most and no further LDS round trip: an entry that is still
+// beyond tlim is visited anyway, which the box tests and the any-order rule
+// make harmless. Returns its reference, or kBvhNone.
 template <class Stk>
 __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t below) {
-    while (T.sp > 0) {
-        const uint32_t key = T.top;
+    if (T.sp == 0) return kBvhNone;
+    uint32_t key = T.top;
+    --T.sp;
+    T.top = below;
+    if (key_tn(key) > T.tlim) {
+        if (T.sp == 0) return kBvhNone;
+        key = T.top;
         --T.sp;
-        T.top = below;
-        if (key_tn(key) <= T.tlim) return key & 0xFFFFu;
-        if (T.sp > 0) below = stack_load(S, T.sp - 1);
+        T.top = stack_load(S, T.sp);  // the entry of depth sp sits in slot sp
+        if (T.sp == 0 && key_tn(key) > T.tlim) return kBvhNone;
     }
-    return kBvhNone;
+    return key & 0xFFFFu;
 }
 
 
@@ -584,14 +614,10 @@ __device__ __forceinline__ void start_sample(const KernelParams& p, UniPtr uni, 
 // ray/tracer.go:143), count its segments, free the lane.
 template <bool kStats>
 __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st) {
-#ifndef TRAY_DIAG_NO_STORE
     double* o = p.samples + (size_t)L.item * 3;
     o[0] = color.x;
     o[1] = color.y;
     o[2] = color.z;
-#else  // diagnostic only: measures what the sample stores cost (wrong images)
-    if (color.x == 12345.0) p.samples[0] = color.y;
-#endif
     if (p.segments) atomicAdd(p.segments + (size_t)L.j * (size_t)p.width + (size_t)L.x, L.segments);
     if constexpr (kStats) st.segments += L.segments;
     L.busy = false;
@@ -663,6 +689,10 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
             ends = true;  // absorbed -> black
         }
     }
+    // Settle the shading-record loads here, on every path: vmcnt is one in-order
+    // counter, so a load still pending when end_path stores would make the next
+    // write of its registers wait for the stores' write-back too.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     if (!ends) return true;
     end_path<kStats>(p, L, color, st);
     return false;
@@ -742,7 +772,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         u->seed = p.seed;
     }
     const UniPtr uni = uni_lds;
-    SceneView sv{p.geo, p.nodes, p.leaves, p.leaf_single != 0, p.bgeo, p.bidx, p.bmat, p.n, p.n_nodes};
+    SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single != 0,       p.bgeo, p.bidx,
+                 p.bmat, p.n,     p.n_nodes,   p.n_global, p.n_slots - p.n_global};
     Stack<kSpill> S{nullptr, nullptr, 0, 0};
     if constexpr (kBVH) {
         // [stacks: stack_cap x blockDim x 4 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]
@@ -803,7 +834,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         uint32_t fresh_item = ~0u;
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
-                const uint32_t c = __shfl(next_chunk, 0);
+                const uint32_t c = __builtin_amdgcn_readlane(next_chunk, 0);
                 if (c >= p.nchunks) {
                     exhausted = true;
                     break;
@@ -828,7 +859,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 start_sample(p, uni, L, fresh_item, x, j, smp);
                 if constexpr (kBVH) {
                     ++L.segments;
-                    trav_begin(T, L.org, L.dir);
+                    trav_begin(T, sv, L.org, L.dir);
+                    if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
                     state = sv.n_nodes > 0 ? kTravState : kShadeState;
                 }
             }
@@ -892,7 +924,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     if (shade_step<kStats>(p, uni, L, T.best, T.closest, [&] { return sv.bgeo[T.slot]; },
                                            [&] { return sv.bmat[T.slot]; }, st)) {
                         ++L.segments;
-                        trav_begin(T, L.org, L.dir);
+                        trav_begin(T, sv, L.org, L.dir);
+                    if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
                         state = sv.n_nodes > 0 ? kTravState : kShadeState;
                     } else {
                         state = kIdleState;

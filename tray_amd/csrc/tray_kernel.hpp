@@ -63,6 +63,7 @@ struct KernelParams {
     const int32_t* bidx;    // original index per slot
     const MatRec* bmat;     // shading record per slot
     int32_t n_nodes, n_slots, n_leaves;
+    int32_t n_global;       // spheres tested before the tree: slots [n_slots - n_global, n_slots)
     int32_t stack_cap;      // traversal stack slots per lane (Bvh::stack_max + 1)
     int32_t stack_lds;      // slots kept in LDS (set by launch_render)
     uint32_t* stack_ovf;    // slots beyond the LDS ones, stride = grid lanes
