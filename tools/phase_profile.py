@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--config", default="c2")
+    ap.add_argument("--shard", default=None, help="N,K: rank K's row tiles of an N-way split (1-row tiles)")
     ap.add_argument("--waves", type=int, default=256 * 16, help="waves in the launch (CUs x waves per CU)")
     args = ap.parse_args()
     import torch
@@ -32,16 +33,21 @@ def main():
     cam.Initialize(W, H)
     scene = _lib.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0, os.path.abspath(args.lib))
     params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
-    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    if args.shard:
+        from tray_amd import shard
+        n, k = (int(v) for v in args.shard.split(","))
+        params = shard.shard_params(params, 1, n, k)
+    out = torch.empty((_lib.params_rows(params), W, 3), dtype=torch.float32, device="cuda")
     stats = torch.zeros(32 + 2 * args.waves, dtype=torch.int64, device="cuda")
     scene.render_stats_async(cam._state, params, out.data_ptr(), stats.data_ptr(),
                              torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     allv = stats.tolist()
-    v = allv[:19]
+    v = allv[:22]
     se = allv[32:]
     names = ["segments", "sphere_tests", "box_tests", "cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade",
-             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "node_leafwait_lanes", "node_shadewait_lanes", "rt_end_max", "rt_life_sum",
+             "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "node_leafwait_lanes", "node_shadewait_lanes", "refill_phases", "refill_lanes",
+             "unused_15", "rt_end_max", "rt_life_sum",
              "rt_start_min_inv"]
     d = dict(zip(names, v))
     cyc = sum(d[k] for k in PHASES)
@@ -51,6 +57,8 @@ def main():
     d["shadewait_lanes_per_node_iter"] = round(d["node_shadewait_lanes"] / max(1, d["node_iters"]), 1)
     d["lanes_per_leaf_phase"] = round(d["leaf_lanes"] / max(1, d["leaf_phases"]), 1)
     d["lanes_per_shade_phase"] = round(d["shade_lanes"] / max(1, d["shade_phases"]), 1)
+    d["lanes_per_refill_phase"] = round(d["refill_lanes"] / max(1, d["refill_phases"]), 1)
+    d["cyc_per_refill_phase"] = round(d["cyc_refill"] / max(1, d["refill_phases"]), 1)
     d["cyc_per_node_iter"] = round(d["cyc_node"] / max(1, d["node_iters"]), 1)
     d["cyc_per_leaf_phase"] = round(d["cyc_leaf"] / max(1, d["leaf_phases"]), 1)
     d["cyc_per_shade_phase"] = round(d["cyc_shade"] / max(1, d["shade_phases"]), 1)

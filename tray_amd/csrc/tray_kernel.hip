@@ -134,6 +134,7 @@ struct Uniforms {
     V3 bg_a, bg_b;
     double focus_time, ray_radius;
     uint64_t seed;
+    uint64_t pool;  // the workgroup's chunk pool: (end << 32) | next (take_chunk)
 };
 // Explicit LDS address space: a generic volatile pointer would be accessed with
 // (slow, system-coherent) flat loads.
@@ -273,9 +274,19 @@ __device__ __forceinline__ void quad(const double4 g, const D3& org, const D3& d
 #endif
 
 // Instrumented launches only: per-lane counters, flushed once when the lane exits.
+#ifndef TRAY_PROFILE
 struct Stats {
     uint64_t segments = 0, spheres = 0, boxes = 0;
 };
+#else  // phase profiles count in LDS; per-lane counters would cost registers
+struct NoCount {
+    __device__ NoCount& operator+=(uint64_t) { return *this; }
+    __device__ operator unsigned long long() const { return 0ull; }
+};
+struct Stats {
+    NoCount segments, spheres, boxes;
+};
+#endif
 
 // Geometry visible to one workgroup (LDS copies, or global memory when the
 // scene does not fit).
@@ -563,6 +574,46 @@ __device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, cons
     return state_of(T.cur);
 }
 
+// Chunks (64 work items each) a workgroup takes from the global queue per atomic.
+// One queue address serves every wave of the device and its atomics serialise
+// there: per-wave fetches left waves waiting on it (1 -> 16 chunks per atomic
+// cut C2 from 11.3 to ~8.4 ms). Waves take single chunks from their workgroup's
+// pool in LDS, so the end of the frame stays balanced at one chunk per wave.
+#ifndef TRAY_POOL_CHUNKS
+#define TRAY_POOL_CHUNKS 16
+#endif
+constexpr uint32_t kPoolDone = 0xFFFFFFFFu;
+
+// The next chunk for this wave (wave-uniform), or kPoolDone once the queue is
+// exhausted. The pool word packs (end << 32) | next: one 64-bit LDS add hands
+// out `next`; the wave that finds next == end refills the pool from the global
+// queue while any other wave that overflowed waits for `end` to change.
+__device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni, uint32_t lane) {
+    typedef __attribute__((address_space(3))) uint64_t LdsU64;
+    LdsU64* pool = (LdsU64*)&uni->pool;
+    const volatile __attribute__((address_space(3))) uint32_t* pool_end =
+        (const volatile __attribute__((address_space(3))) uint32_t*)&uni->pool + 1;
+    while (true) {
+        uint64_t old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(pool, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t next = __builtin_amdgcn_readlane((uint32_t)old, 0);
+        const uint32_t end = __builtin_amdgcn_readlane((uint32_t)(old >> 32), 0);
+        if (end == kPoolDone) return kPoolDone;
+        if (next < end) return next;
+        if (next == end) {  // first past the end: refill
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(p.queue, (uint32_t)TRAY_POOL_CHUNKS);
+            base = __builtin_amdgcn_readlane(base, 0);
+            const uint64_t fresh = base >= p.nchunks
+                                       ? (uint64_t)kPoolDone << 32
+                                       : ((uint64_t)min(base + (uint32_t)TRAY_POOL_CHUNKS, p.nchunks) << 32) | base;
+            if (lane == 0) __hip_atomic_store(pool, fresh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            continue;
+        }
+        while (__builtin_amdgcn_readlane(*pool_end, 0) == end) __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 // Work item i of a band = one sample: pixel q = i / r in 8x8-tile order of the
 // band's compact rows (so a 64-item chunk is one pixel's samples at r = 64, or
 // an 8x8 tile at r = 1), sample s = i % r.
@@ -720,12 +771,18 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 
 // Diagnostic build only (-DTRAY_PROFILE): per-wave s_memtime stamps around each
 // phase of the BVH loop, plus phase and active-lane counts, added into
-// stats[3..18] (the stats buffer must then hold 19 counters). Never part of a
+// stats[3..21] (the stats buffer must then hold 22 counters). Never part of a
 // timed build: the stamps' waits serialise the phases.
 #ifdef TRAY_PROFILE
+// Counters live in LDS (per wave, lane 0 adds): registers would change the
+// kernel being measured.
 #define PROF_T0() const uint64_t prof_t0_ = __builtin_amdgcn_s_memtime()
-#define PROF_ADD(slot) prof[slot] += __builtin_amdgcn_s_memtime() - prof_t0_
-#define PROF_CNT(slot, v) prof[slot] += (v)
+#define PROF_ADD(slot) PROF_CNT(slot, __builtin_amdgcn_s_memtime() - prof_t0_)
+#define PROF_CNT(slot, v)                                  \
+    {                                                      \
+        const unsigned long long v_ = (v);                 \
+        if (lane == 0) atomicAdd(prof + (slot), v_);       \
+    }
 #else
 #define PROF_T0()
 #define PROF_ADD(slot)
@@ -770,6 +827,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         u->focus_time = p.focus_time;
         u->ray_radius = p.ray_radius;
         u->seed = p.seed;
+        u->pool = 0;  // empty: the first taker refills it
     }
     const UniPtr uni = uni_lds;
     SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single != 0,       p.bgeo, p.bidx,
@@ -815,11 +873,12 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     Trav T;
     uint32_t state = kIdleState;
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
-    uint32_t next_chunk = 0;                // lane 0: the wave's next chunk, fetched ahead
-    if (lane == 0) next_chunk = atomicAdd(p.queue, 1u);
     bool exhausted = false;
 #ifdef TRAY_PROFILE
-    uint64_t prof[16] = {};
+    __shared__ unsigned long long prof_lds[16 * 16];
+    unsigned long long* prof = prof_lds + 16 * (threadIdx.x / 64u);
+    if (lane == 0)
+        for (int i = 0; i < 16; ++i) prof[i] = 0;
     const uint64_t prof_start = __builtin_amdgcn_s_memrealtime();
 #endif
 
@@ -834,12 +893,11 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         uint32_t fresh_item = ~0u;
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
-                const uint32_t c = __builtin_amdgcn_readlane(next_chunk, 0);
-                if (c >= p.nchunks) {
+                const uint32_t c = take_chunk(p, uni, lane);
+                if (c == kPoolDone) {
                     exhausted = true;
                     break;
                 }
-                if (lane == 0) next_chunk = atomicAdd(p.queue, 1u);  // prefetch the one after
                 pool_next = c * 64u;
                 pool_end = pool_next + 64u;
             }
@@ -852,6 +910,13 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             pool_next += take;
             idle = __ballot(!L.busy && fresh_item == ~0u);
         }
+#ifdef TRAY_PROFILE
+        {
+            const uint64_t fresh = __ballot(fresh_item != ~0u);
+            PROF_CNT(13, fresh != 0ull ? 1 : 0);
+            PROF_CNT(14, __popcll(fresh));
+        }
+#endif
         if (fresh_item != ~0u) {
             int32_t x, j;
             uint32_t smp;
@@ -867,7 +932,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         }
         PROF_ADD(0);
         if (__ballot(L.busy) == 0ull) {
-            if (exhausted) break;  // (a prefetched chunk must not be dropped)
+            if (exhausted) break;
             continue;              // every lane drew a padding item: draw again
         }
 
@@ -942,12 +1007,12 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     }
 #ifdef TRAY_PROFILE
     if (kStats && lane == 0) {
-        for (int i = 0; i < 13; ++i) atomicAdd(p.stats + 3 + i, (unsigned long long)prof[i]);
+        for (int i = 0; i < 16; ++i) atomicAdd(p.stats + 3 + i, (unsigned long long)prof[i]);
         // Wave lifetimes on the constant-rate clock: latest exit, sum of lifetimes, earliest start.
         const uint64_t end = __builtin_amdgcn_s_memrealtime();
-        atomicMax(p.stats + 16, (unsigned long long)end);
-        atomicAdd(p.stats + 17, (unsigned long long)(end - prof_start));
-        atomicMax(p.stats + 18, (unsigned long long)~prof_start);
+        atomicMax(p.stats + 19, (unsigned long long)end);
+        atomicAdd(p.stats + 20, (unsigned long long)(end - prof_start));
+        atomicMax(p.stats + 21, (unsigned long long)~prof_start);
         // Per-wave (start, end) from stats[32] on (the buffer must hold 32 + 2 x waves).
         const uint32_t wave = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
         p.stats[32 + 2 * wave] = prof_start;

@@ -16,7 +16,11 @@ enum : int32_t { kOutRGBF64 = 0, kOutRGBF32 = 1, kOutRGBA8 = 2 };
 // Sphere geometry is staged into LDS as double4 {cx, cy, cz, R*R} (32 B).
 // Up to 160 KiB of LDS per workgroup on gfx950 -> 5120 spheres; larger scenes
 // read the same array from global memory (L2/L1-resident).
+#ifdef TRAY_PROFILE
+constexpr size_t kMaxLDSBytes = 158 * 1024;  // diagnostic builds keep 2 KB of counters in LDS
+#else
 constexpr size_t kMaxLDSBytes = 160 * 1024;
+#endif
 
 // Per-sphere shading record, read only for the closest hit (64 B).
 struct MatRec {
