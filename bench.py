@@ -11,6 +11,12 @@ row tiles (default 1 row: rank k renders rows y = k mod N; one shard per rank,
 no collective inside the render) and the step
 ends with ONE RCCL gather of the row tiles to rank 0 ("scaling": "strong": the
 frame is fixed as N grows). value = W*H*r*steps / max-over-ranks wall time.
+Consecutive steps overlap three deep by default (--frames-in-flight): each frame
+slot has its own device scene (work queue, sample buffer), output and stream,
+so frame i+1's workgroups start on the CUs that frame i's last long paths
+(up to d=50 segments, ~0.3 ms of latency) leave idle; every step still renders
+its whole frame inside the timed region. --frames-in-flight 1 times frames
+back to back.
 
 Also reported (rank 0):
   roofline     the megakernel against the FP64 VALU roof (it is compute and
@@ -71,6 +77,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-step", type=int, default=1, help="oracle renders every k-th row of the frame")
     ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")
+    ap.add_argument("--frames-in-flight", type=int, default=3,
+                    help="consecutive steps overlap this deep (own scene copy, output and stream each): "
+                         "a frame's blocks start on CUs the previous frame's last paths leave idle")
     args = ap.parse_args()
 
     import torch
@@ -94,21 +103,28 @@ def main() -> int:
     cam = ray.RichSceneCamera()
     cam.Initialize(W, H)
     bg = ray._background(ray.DefaultBackground())
-    scene = _lib.DeviceScene(spheres, bg, local_rank)
     params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32,
                               flags=_lib.FLAG_LINEAR_SCAN if args.linear else 0)
     params = shard.shard_params(params, args.tile_rows, world, rank)
     rows = _lib.params_rows(params)
-    out = torch.empty((rows, W, 3), dtype=torch.float32, device="cuda")
-    stream = torch.cuda.current_stream()
+    # Frame slots: step i renders in slot i % F (its own device scene - work
+    # queue and sample buffer -, output and stream), so step i+1 starts while
+    # step i's slowest paths and its gather finish.
+    nslot = max(1, args.frames_in_flight)
+    scenes = [_lib.DeviceScene(spheres, bg, local_rank) for _ in range(nslot)]
+    outs = [torch.empty((rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslot - 1)]
+    scene, out, stream = scenes[0], outs[0], streams[0]
 
-    def render(seg_ptr=None):
-        scene.render_async(cam._state, params, out.data_ptr(), seg_ptr, stream.cuda_stream)
+    def render(k=0, seg_ptr=None):
+        scenes[k].render_async(cam._state, params, outs[k].data_ptr(), seg_ptr, streams[k].cuda_stream)
 
-    def step():
-        render()
-        if world > 1:
-            shard.gather_image(out, H, args.tile_rows, world, rank)
+    def step(i):
+        k = i % nslot
+        with torch.cuda.stream(streams[k]):
+            render(k)
+            if world > 1:
+                shard.gather_image(outs[k], H, args.tile_rows, world, rank)
 
     # Untimed instrumented launch: segments, ray-sphere and ray-box tests for the roofline.
     stats = torch.zeros(3, dtype=torch.int64, device="cuda")
@@ -116,25 +132,28 @@ def main() -> int:
     torch.cuda.synchronize()
     segments_local, sphere_tests, box_tests = (int(v) for v in stats.tolist())
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        render()
-        ev[i][1].record(stream)
-        if world > 1:
-            shard.gather_image(out, H, args.tile_rows, world, rank)
+        step(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # Untimed: one frame at a time, HIP events on the launch stream, for the
+    # roofline's per-launch duration.
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+    for a, b in ev:
+        a.record(stream)
+        render(0)
+        b.record(stream)
+    torch.cuda.synchronize()
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -163,6 +182,7 @@ def main() -> int:
             "width": W, "height": H, "rays_per_pixel": spp, "max_depth": depth, "scene_seed": seed,
             "spheres": int(len(spheres)), "output": "float3 f32 linear", "parallelism": f"row-tiles x{world}",
             "tile_rows": args.tile_rows if world > 1 else 0,
+            "frames_in_flight": nslot,
         },
     }
     if rank == 0:
@@ -210,7 +230,8 @@ def main() -> int:
             rec["cpu_baseline"] = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed,
                                                args.cpu_row_step)
     print(json.dumps(rec), flush=True)
-    scene.release()
+    for sc in scenes:
+        sc.release()
     if dist:
         dist.destroy_process_group()
     return 0

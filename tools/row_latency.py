@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--rows", default="0,100,300,360,420,600,700")
     ap.add_argument("--count", type=int, default=1)
+    ap.add_argument("--depths", default=None, help="comma list of max depths to sweep (default: the config's)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--lib", default=None, help="a libtray_amd.so build to load (default: the in-tree one)")
     args = ap.parse_args()
@@ -36,7 +37,8 @@ def main():
     lib = os.path.abspath(args.lib) if args.lib else None
     scene = _lib.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0, *([lib] if lib else []))
     stream = torch.cuda.current_stream()
-    for y0 in [int(v) for v in args.rows.split(",")]:
+    depths = [int(v) for v in args.depths.split(",")] if args.depths else [depth]
+    for y0, depth in [(y, d) for y in (int(v) for v in args.rows.split(",")) for d in depths]:
         p = _lib.make_params(W, H, depth, spp, 0.5, seed, y_start=y0, y_end=y0 + args.count,
                              output=_lib.OUT_RGB_F32)
         out = torch.empty((args.count, W, 3), dtype=torch.float32, device="cuda")
@@ -52,7 +54,7 @@ def main():
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b))
         s = seg.cpu().numpy().astype(np.float64) / spp
-        print(json.dumps({"y0": y0, "rows": args.count, "ms": round(float(np.median(ts)), 4),
+        print(json.dumps({"y0": y0, "rows": args.count, "depth": depth, "ms": round(float(np.median(ts)), 4),
                           "seg_per_sample_mean": round(float(s.mean()), 3),
                           "pixel_mean_seg_max": round(float(s.max()), 3)}), flush=True)
 

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--tile-rows", type=int, default=1)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--frames-in-flight", type=int, default=1,
+                    help="> 1: time --reps consecutive frames per shard overlapped this deep (bench.py's default is 3)")
     ap.add_argument("--lib", default=None, help="a libtray_amd.so build to load (default: the in-tree one)")
     args = ap.parse_args()
     import numpy as np
@@ -39,7 +41,37 @@ def main():
     stream = torch.cuda.current_stream()
     base = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
 
+    nslot = max(1, args.frames_in_flight)
+    extra = [_lib.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0, *([lib] if lib else []))
+             for _ in range(nslot - 1)]
+    streams = [torch.cuda.Stream() for _ in range(nslot)]
+
+    def time_pipelined(n, k):
+        p = shard.shard_params(base, args.tile_rows, n, k)
+        outs = [torch.empty((_lib.params_rows(p), W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
+        scs = [scene] + extra
+        for i in range(nslot):  # warm
+            scs[i].render_async(cam._state, p, outs[i].data_ptr(), None, streams[i].cuda_stream)
+        torch.cuda.synchronize()
+        reps = max(args.reps, 4 * nslot)
+        a = torch.cuda.Event(enable_timing=True)
+        a.record(torch.cuda.current_stream())
+        for s_ in streams:
+            s_.wait_event(a)
+        for i in range(reps):
+            j = i % nslot
+            scs[j].render_async(cam._state, p, outs[j].data_ptr(), None, streams[j].cuda_stream)
+        ends = []
+        for s_ in streams:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(s_)
+            ends.append(e)
+        torch.cuda.synchronize()
+        return max(a.elapsed_time(e) for e in ends) / reps
+
     def time_shard(n, k):
+        if nslot > 1:
+            return time_pipelined(n, k)
         p = shard.shard_params(base, args.tile_rows, n, k)
         out = torch.empty((_lib.params_rows(p), W, 3), dtype=torch.float32, device="cuda")
         scene.render_async(cam._state, p, out.data_ptr(), None, stream.cuda_stream)  # warm
@@ -58,7 +90,7 @@ def main():
         times = [time_shard(n, k) for k in range(n)]
         if n == 1:
             t1 = times[0]
-        rec = {"config": args.config, "n": n, "tile_rows": args.tile_rows, "max_ms": round(max(times), 4),
+        rec = {"config": args.config, "n": n, "tile_rows": args.tile_rows, "frames_in_flight": nslot, "max_ms": round(max(times), 4),
                "min_ms": round(min(times), 4), "mean_ms": round(float(np.mean(times)), 4)}
         if t1:
             rec["render_efficiency"] = round(t1 / (n * max(times)), 4)

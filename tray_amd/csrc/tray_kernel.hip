@@ -756,7 +756,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 // be waiting before the (expensive, FP64) leaf and shading phases run. A phase
 // also runs whenever nothing else can make progress.
 #ifndef TRAY_NODE_STEPS
-#define TRAY_NODE_STEPS 1
+#define TRAY_NODE_STEPS 3
 #endif
 #ifndef TRAY_LEAF_BATCH
 #define TRAY_LEAF_BATCH 24
@@ -766,7 +766,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #endif
 // Idle lanes are refilled (a camera ray each) once this many wait, or the whole wave does.
 #ifndef TRAY_REFILL_BATCH
-#define TRAY_REFILL_BATCH 16
+#define TRAY_REFILL_BATCH 24
 #endif
 
 // Diagnostic build only (-DTRAY_PROFILE): per-wave s_memtime stamps around each

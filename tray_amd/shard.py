@@ -54,6 +54,18 @@ def gather_image(local, height: int, tile_rows: int, world: int, rank: int, dst:
         return None
     full = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     for r in range(world):
-        idx = torch.as_tensor(rows_for(height, tile_rows, world, r), dtype=torch.long, device=local.device)
-        full.index_copy_(0, idx, bufs[r][: counts[r]])
+        full.index_copy_(0, _row_index(height, tile_rows, world, r, local.device), bufs[r][: counts[r]])
     return full
+
+
+_ROW_INDEX = {}
+
+
+def _row_index(height, tile_rows, world, rank, device):
+    """Device tensor of rows_for(...), built once (no host copy per gather)."""
+    import torch
+
+    key = (height, tile_rows, world, rank, str(device))
+    if key not in _ROW_INDEX:
+        _ROW_INDEX[key] = torch.as_tensor(rows_for(height, tile_rows, world, rank), dtype=torch.long, device=device)
+    return _ROW_INDEX[key]
