@@ -132,6 +132,8 @@ def main() -> int:
     torch.cuda.synchronize()
     segments_local, sphere_tests, box_tests = (int(v) for v in stats.tolist())
 
+    for k in range(nslot):  # setup: each slot's sample buffer and launch state
+        render(k)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
