@@ -358,12 +358,9 @@ struct Trav {
     int32_t slot;  // its leaf slot (geometry + shading record)
 };
 
-#ifndef TRAY_BVH_WAVES_PER_SIMD
-#define TRAY_BVH_WAVES_PER_SIMD 4
-#endif
-// The BVH kernel runs one workgroup per CU (all its waves share one LDS copy of
-// the scene); the linear scan runs 256-lane workgroups.
-constexpr int kBvhBlock = 256 * TRAY_BVH_WAVES_PER_SIMD;
+// The BVH kernel runs one workgroup per CU by default (all its waves share one
+// LDS copy of the scene); the linear scan runs 256-lane workgroups.
+constexpr int kBvhBlock = TRAY_BVH_BLOCK;
 static_assert(kBvhBlock <= 1024, "BVH workgroup larger than 1024 lanes");
 // Traversal stack slots per lane are kept in LDS as far as the workgroup's LDS
 // allows after the scene (4 KB per slot), at least kStackLdsMin of them.

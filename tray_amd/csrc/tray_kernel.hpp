@@ -16,10 +16,19 @@ enum : int32_t { kOutRGBF64 = 0, kOutRGBF32 = 1, kOutRGBA8 = 2 };
 // Sphere geometry is staged into LDS as double4 {cx, cy, cz, R*R} (32 B).
 // Up to 160 KiB of LDS per workgroup on gfx950 -> 5120 spheres; larger scenes
 // read the same array from global memory (L2/L1-resident).
+// BVH workgroups: TRAY_BVH_BLOCK lanes each, TRAY_BVH_WAVES_PER_SIMD waves per
+// SIMD, so (4 SIMDs x waves x 64) / block workgroups share a CU and its LDS.
+#ifndef TRAY_BVH_WAVES_PER_SIMD
+#define TRAY_BVH_WAVES_PER_SIMD 4
+#endif
+#ifndef TRAY_BVH_BLOCK
+#define TRAY_BVH_BLOCK (256 * TRAY_BVH_WAVES_PER_SIMD)
+#endif
+constexpr int kBvhBlocksPerCU = 256 * TRAY_BVH_WAVES_PER_SIMD / TRAY_BVH_BLOCK;
 #ifdef TRAY_PROFILE
-constexpr size_t kMaxLDSBytes = 158 * 1024;  // diagnostic builds keep 2 KB of counters in LDS
+constexpr size_t kMaxLDSBytes = (160 * 1024) / kBvhBlocksPerCU - 2048;  // diagnostic builds: 2 KB of counters
 #else
-constexpr size_t kMaxLDSBytes = 160 * 1024;
+constexpr size_t kMaxLDSBytes = (160 * 1024) / kBvhBlocksPerCU;
 #endif
 
 // Per-sphere shading record, read only for the closest hit (64 B).
