@@ -25,12 +25,16 @@ struct Block {
     uint32_t x0, x1, x2, x3;
 };
 
-// Philox4x32-10 (Salmon et al. 2011, Random123 constants).
+// Philox4x32-10 (Salmon et al. 2011, Random123 constants). TRAY_PHILOX_ROUNDS
+// exists only for cost experiments (tools/build_variants.sh); the contract is 10.
+#ifndef TRAY_PHILOX_ROUNDS
+#define TRAY_PHILOX_ROUNDS 10
+#endif
 __host__ __device__ __forceinline__ Block philox4x32_10(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2,
                                                         uint32_t c3) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < TRAY_PHILOX_ROUNDS; ++r) {
         if (r > 0) {
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
