@@ -37,10 +37,15 @@
  *     UnitVector  = z = 1 - 2 u0, s = sqrt(1 - z*z), (s cos(2 pi u1), s sin(2 pi u1), z)
  *     Float64     = u0 of the scatter block (Dielectric, ray/materials.go:57)
  * where sin/cos(2 pi u) is "sincos2pi": quadrant q = floor(4u), f = 4u - q
- * reflected into [0, 0.5], t = f * (pi/2), Taylor polynomials in t^2 of degree
- * 15 (sin) and 16 (cos) in Horner form, then the quadrant rotation
- * (tray_amd/csrc/rng.hpp). Only + - * / sqrt are used, in a fixed order, so the
- * host oracle and the device produce identical bits.
+ * reflected into [0, 0.5] (exact, FP64), then in FP32: t = RN32(f) * RN32(pi/2),
+ * Taylor polynomials in t^2 of degree 9 (sin) and 10 (cos) by Horner's rule
+ * with correctly rounded fmaf; back in FP64 one Newton step onto the unit
+ * circle, k = 1.5 - 0.5 (s^2 + c^2), (s, c) *= k, then the quadrant rotation
+ * (tray_amd/csrc/rng.hpp). The angle is accurate to ~1e-7, the length s^2 + c^2
+ * to ~1e-14. IEEE FP32 with fmaf, in a fixed
+ * order, gives identical bits on the host oracle and the device. (FP32 and
+ * fma appear only in this sampler transform; the reference arithmetic of
+ * ray/vec3.go, objects.go, materials.go and camera.go is FP64, uncontracted.)
  * A given (seed, pixel, sample) therefore renders the same colour for any
  * tiling, row range, device count or launch geometry.
  */

@@ -170,43 +170,43 @@ static void uniforms2(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint
     u[1] = (double)(b >> 11) * 0x1.0p-53;
 }
 
-/* sin and cos of 2*pi*u for u in [0,1), with + and * only in a fixed order
- * (include/tray.h "sincos2pi"): quadrant + reflection into [0, pi/4], then
- * Taylor polynomials (degree 15 / 16) in Horner form. Same bits on any IEEE
- * double machine without contraction. */
+/* sin and cos of 2*pi*u for u in [0,1) (include/tray.h "sincos2pi"): exact
+ * FP64 quadrant + reflection into [0, 1/2], then FP32 Taylor polynomials
+ * (degree 9 / 10) in t^2 by Horner's rule with C99 fmaf() (correctly rounded,
+ * as the device's v_fma_f32), so both sides produce the same bits. This is the
+ * contract's sampler transform, not reference arithmetic: ray/rand.go:30-32
+ * delegates to fortio.org/rand, whose stream cannot be reproduced. Needs
+ * FLT_EVAL_METHOD 0 (SSE float arithmetic, the x86-64 default). */
 static void sincos_2pi(double u, double *s, double *c) {
     double v = u * 4.0;
     double q = floor(v);
     double f = v - q;
     int quad = (int)q;
     int swap = f > 0.5;
-    double x = swap ? 1.0 - f : f;
-    double t = x * 0x1.921fb54442d18p+0; /* pi/2 */
-    double t2 = t * t;
-    double sp = -0x1.ae7f3e733b81fp-41;         /* -1/15! */
-    sp = sp * t2 + 0x1.6124613a86d09p-33;       /* 1/13! */
-    sp = sp * t2 + -0x1.ae64567f544e4p-26;      /* -1/11! */
-    sp = sp * t2 + 0x1.71de3a556c734p-19;       /* 1/9! */
-    sp = sp * t2 + -0x1.a01a01a01a01ap-13;      /* -1/7! */
-    sp = sp * t2 + 0x1.1111111111111p-7;        /* 1/5! */
-    sp = sp * t2 + -0x1.5555555555555p-3;       /* -1/3! */
-    sp = sp * t2 + 1.0;
-    double sn = t * sp;
-    double cp = 0x1.ae7f3e733b81fp-45;          /* 1/16! */
-    cp = cp * t2 + -0x1.93974a8c07c9dp-37;      /* -1/14! */
-    cp = cp * t2 + 0x1.1eed8eff8d898p-29;       /* 1/12! */
-    cp = cp * t2 + -0x1.27e4fb7789f5cp-22;      /* -1/10! */
-    cp = cp * t2 + 0x1.a01a01a01a01ap-16;       /* 1/8! */
-    cp = cp * t2 + -0x1.6c16c16c16c17p-10;      /* -1/6! */
-    cp = cp * t2 + 0x1.5555555555555p-5;        /* 1/4! */
-    cp = cp * t2 + -0.5;                        /* -1/2! */
-    double cs = cp * t2 + 1.0;
-    if (swap) { double tmp = sn; sn = cs; cs = tmp; }
+    float x = (float)(swap ? 1.0 - f : f);
+    float t = x * 0x1.921fb6p+0f; /* RN32(pi/2) */
+    float t2 = t * t;
+    float sp = fmaf(t2, 0x1.71de3ap-19f, -0x1.a01a02p-13f); /* 1/9!, -1/7! */
+    sp = fmaf(sp, t2, 0x1.111112p-7f);                       /* 1/5! */
+    sp = fmaf(sp, t2, -0x1.555556p-3f);                      /* -1/3! */
+    sp = fmaf(sp, t2, 1.0f);
+    float sn = t * sp;
+    float cp = fmaf(t2, -0x1.27e4fcp-22f, 0x1.a01a02p-16f); /* -1/10!, 1/8! */
+    cp = fmaf(cp, t2, -0x1.6c16c2p-10f);                     /* -1/6! */
+    cp = fmaf(cp, t2, 0x1.555556p-5f);                       /* 1/4! */
+    cp = fmaf(cp, t2, -0.5f);
+    float cs = fmaf(cp, t2, 1.0f);
+    if (swap) { float tmp = sn; sn = cs; cs = tmp; }
+    /* one FP64 Newton step onto the unit circle (unit vectors are pinned to
+     * 1e-9 by ray/vec3_test.go:505-537) */
+    double sd = sn, cd = cs;
+    double k = 1.5 - 0.5 * (sd * sd + cd * cd);
+    double sk = sd * k, ck = cd * k;
     switch (quad & 3) {
-    case 0: *s = sn; *c = cs; break;
-    case 1: *s = cs; *c = -sn; break;
-    case 2: *s = -sn; *c = -cs; break;
-    default: *s = -cs; *c = sn; break;
+    case 0: *s = sk; *c = ck; break;
+    case 1: *s = ck; *c = -sk; break;
+    case 2: *s = -sk; *c = -ck; break;
+    default: *s = -ck; *c = sk; break;
     }
 }
 

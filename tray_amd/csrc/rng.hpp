@@ -70,45 +70,48 @@ __host__ __device__ __forceinline__ U4 philox_u4(uint64_t seed, uint32_t c0, uin
               (double)b.x3 * 0x1.0p-32};
 }
 
-// sin and cos of 2*pi*u, u in [0,1), with + and * only in a fixed order (the
-// "sincos2pi" of include/tray.h): quadrant and reflection into [0, pi/4], then
-// Taylor polynomials of degree 15 (sin) and 16 (cos) in Horner form. Built
-// with -ffp-contract=off this gives the same bits on the host and the device.
+// sin and cos of 2*pi*u, u in [0,1) (the "sincos2pi" of include/tray.h). The
+// quadrant and the reflection into [0, 1/2] are exact in FP64; the polynomial
+// runs in FP32: t = RN32(x) * RN32(pi/2), then Taylor polynomials of degree 9
+// (sin) and 10 (cos) in t^2 by Horner's rule with correctly rounded fmaf. Both
+// are accurate to ~1e-7, far finer than anything a sampled direction feeds
+// (the uniforms themselves are 32-bit), and IEEE FP32 + fmaf give the same bits
+// on the host oracle and the device. This is the contract's sampler transform,
+// not reference arithmetic (which stays FP64, uncontracted): the FP64 form cost
+// ~40 FP64 instructions and its registers, 3.5 % of the C2 frame.
 __host__ __device__ __forceinline__ void sincos_2pi(double u, double& s, double& c) {
     const double v = u * 4.0;
     const double q = __builtin_floor(v);
     const double f = v - q;
     const int quad = (int)q;
     const bool swap = f > 0.5;
-    const double x = swap ? 1.0 - f : f;
-    const double t = x * 0x1.921fb54442d18p+0;  // pi/2
-    const double t2 = t * t;
-    double sp = -0x1.ae7f3e733b81fp-41;
-    sp = sp * t2 + 0x1.6124613a86d09p-33;
-    sp = sp * t2 + -0x1.ae64567f544e4p-26;
-    sp = sp * t2 + 0x1.71de3a556c734p-19;
-    sp = sp * t2 + -0x1.a01a01a01a01ap-13;
-    sp = sp * t2 + 0x1.1111111111111p-7;
-    sp = sp * t2 + -0x1.5555555555555p-3;
-    sp = sp * t2 + 1.0;
-    double sn = t * sp;
-    double cp = 0x1.ae7f3e733b81fp-45;
-    cp = cp * t2 + -0x1.93974a8c07c9dp-37;
-    cp = cp * t2 + 0x1.1eed8eff8d898p-29;
-    cp = cp * t2 + -0x1.27e4fb7789f5cp-22;
-    cp = cp * t2 + 0x1.a01a01a01a01ap-16;
-    cp = cp * t2 + -0x1.6c16c16c16c17p-10;
-    cp = cp * t2 + 0x1.5555555555555p-5;
-    cp = cp * t2 + -0.5;
-    double cs = cp * t2 + 1.0;
+    const float x = (float)(swap ? 1.0 - f : f);
+    const float t = x * 0x1.921fb6p+0f;  // RN32(pi/2)
+    const float t2 = t * t;
+    float sp = __builtin_fmaf(t2, 0x1.71de3ap-19f, -0x1.a01a02p-13f);  // 1/9!, -1/7!
+    sp = __builtin_fmaf(sp, t2, 0x1.111112p-7f);                        // 1/5!
+    sp = __builtin_fmaf(sp, t2, -0x1.555556p-3f);                       // -1/3!
+    sp = __builtin_fmaf(sp, t2, 1.0f);
+    float sn = t * sp;
+    float cp = __builtin_fmaf(t2, -0x1.27e4fcp-22f, 0x1.a01a02p-16f);  // -1/10!, 1/8!
+    cp = __builtin_fmaf(cp, t2, -0x1.6c16c2p-10f);                      // -1/6!
+    cp = __builtin_fmaf(cp, t2, 0x1.555556p-5f);                        // 1/4!
+    cp = __builtin_fmaf(cp, t2, -0.5f);
+    float cs = __builtin_fmaf(cp, t2, 1.0f);
     if (swap) {
-        const double tmp = sn;
+        const float tmp = sn;
         sn = cs;
         cs = tmp;
     }
+    // One FP64 Newton step onto the unit circle, k = 1.5 - 0.5 (s^2 + c^2):
+    // |(s, c)| = 1 within ~1e-14 (ray/vec3_test.go:505-537 pins unit vectors
+    // to 1e-9; the FP32 pair alone is only within ~1e-7).
+    const double sd = sn, cd = cs;
+    const double k = 1.5 - 0.5 * (sd * sd + cd * cd);
+    const double sk = sd * k, ck = cd * k;
     const int qq = quad & 3;
-    s = qq == 0 ? sn : qq == 1 ? cs : qq == 2 ? -sn : -cs;
-    c = qq == 0 ? cs : qq == 1 ? -sn : qq == 2 ? -cs : sn;
+    s = qq == 0 ? sk : qq == 1 ? ck : qq == 2 ? -sk : -ck;
+    c = qq == 0 ? ck : qq == 1 ? -sk : qq == 2 ? -ck : sk;
 }
 
 }  // namespace tray

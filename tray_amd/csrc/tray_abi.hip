@@ -89,8 +89,8 @@ static int device_state(int32_t device, DeviceState** out) {
 }  // namespace tray
 
 // A scene resident on one device. Renders of one scene handle share its work
-// queue counter, so they must be ordered on one stream (the queue is re-zeroed
-// by every launch).
+// queue counter, so they must be ordered on one stream (the queue is zero when
+// a launch starts: zeroed at allocation, then by each band's resolve pass).
 struct tray_scene_s {
     int32_t device;
     int32_t n;
@@ -275,6 +275,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->bg_b = V3{bg->color_b[0], bg->color_b[1], bg->color_b[2]};
     hipError_t e = hipMalloc(&sc->geo, sizeof(double4) * (size_t)n_pad);
     if (e == hipSuccess) e = hipMalloc(&sc->queue, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(sc->queue, 0, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemcpy(sc->geo, geo.data(), sizeof(double4) * (size_t)n_pad, hipMemcpyHostToDevice);
     if (e == hipSuccess && n > 0) e = hipMalloc(&sc->mat, sizeof(MatRec) * (size_t)n);
     if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);

@@ -60,7 +60,7 @@ struct V3 {
 struct KernelParams {
     const double4* geo;  // n_pad entries: n spheres, then NaN padding (never hit)
     const MatRec* mat;
-    uint32_t* queue;     // work-item counter, zeroed before every launch
+    uint32_t* queue;     // work-item counter: zero at launch (allocation, then each resolve pass)
     int32_t n;
     int32_t n_pad;       // round_up(n, 4) + 4
     int32_t tiles_x;     // 8x8 pixel tiles per compact row band
