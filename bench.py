@@ -5,18 +5,22 @@ headline workload (config 2: book-cover scene, seed 2, 1280x720, r=64, d=50).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-A step = one full frame rendered through the C-ABI (tray_render_async) with the
-scene already resident in HBM; for N > 1 the frame is split into interleaved
-row tiles (default 1 row: rank k renders rows y = k mod N; one shard per rank,
-no collective inside the render) and the step
-ends with ONE RCCL gather of the row tiles to rank 0 ("scaling": "strong": the
-frame is fixed as N grows). value = W*H*r*steps / max-over-ranks wall time.
-Consecutive steps overlap three deep by default (--frames-in-flight): each frame
-slot has its own device scene (work queue, sample buffer), output and stream,
-so frame i+1's workgroups start on the CUs that frame i's last long paths
-(up to d=50 segments, ~0.3 ms of latency) leave idle; every step still renders
-its whole frame inside the timed region. --frames-in-flight 1 times frames
-back to back.
+A step = one full frame rendered through the C-ABI with the scene already
+resident in HBM; for N > 1 the frame is split into interleaved row tiles
+(default 1 row: rank k renders rows y = k mod N; one shard per rank, no
+collective inside the render) and the frames are gathered to rank 0 by RCCL
+over xGMI ("scaling": "strong": the frame is fixed as N grows).
+value = W*H*r*steps / max-over-ranks wall time.
+Frames are progressive passes (tray_params.pass = frame index: every frame
+draws fresh samples). --passes F renders F frames per launch
+(tray_render_passes_async: lanes flow from one frame's samples into the next,
+so a launch has one tail of long paths, not F; default 1 at N = 1, 8 at N > 1,
+where a shard is ~1 ms of work and a d=50 tail would cost ~10 %), with ONE
+gather per launch. Launches rotate over --frames-in-flight slots (own device
+scene - work queue, sample buffer -, output and stream; default 3 at F = 1,
+else 2), so a launch's workgroups start on the CUs the previous launch's last
+long paths leave idle. Every step still renders its whole frame inside the
+timed region.
 
 Also reported (rank 0):
   roofline     the megakernel against the FP64 VALU roof (it is compute and
@@ -77,9 +81,13 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-step", type=int, default=1, help="oracle renders every k-th row of the frame")
     ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")
-    ap.add_argument("--frames-in-flight", type=int, default=3,
-                    help="consecutive steps overlap this deep (own scene copy, output and stream each): "
-                         "a frame's blocks start on CUs the previous frame's last paths leave idle")
+    ap.add_argument("--frames-in-flight", type=int, default=None,
+                    help="launches overlap this deep (own scene copy, output and stream each): a launch's "
+                         "blocks start on CUs the previous launch's last paths leave idle "
+                         "(default 3 with one frame per launch, else 2)")
+    ap.add_argument("--passes", type=int, default=None,
+                    help="frames per launch (tray_render_passes_async: consecutive progressive passes, one "
+                         "persistent launch, no per-frame tail); default 1 at N = 1, 8 at N > 1")
     args = ap.parse_args()
 
     import torch
@@ -87,6 +95,11 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # TRAY_BENCH_BACKEND=gloo rehearses the N > 1 code path on ONE GPU (ranks
+    # share device 0; RCCL refuses two ranks on one device). Never for numbers.
+    backend = os.environ.get("TRAY_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local_rank = 0
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
     torch.cuda.set_device(local_rank)
@@ -94,7 +107,10 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     from tray_amd import _lib, ray, shard
 
@@ -107,53 +123,72 @@ def main() -> int:
                               flags=_lib.FLAG_LINEAR_SCAN if args.linear else 0)
     params = shard.shard_params(params, args.tile_rows, world, rank)
     rows = _lib.params_rows(params)
-    # Frame slots: step i renders in slot i % F (its own device scene - work
-    # queue and sample buffer -, output and stream), so step i+1 starts while
-    # step i's slowest paths and its gather finish.
-    nslot = max(1, args.frames_in_flight)
+    # A step is one frame. Frames are rendered F per launch (progressive passes
+    # of tray_render_passes_async: lanes flow from one frame's samples into the
+    # next, so a launch has one tail of long paths, not F), and launches
+    # rotate over frame slots (own device scene - work queue and sample
+    # buffer -, output and stream), so launch j+1 starts on the CUs launch j's
+    # last paths leave idle. A small shard (N > 1) is dominated by those tails.
+    F = args.passes if args.passes else (1 if world == 1 else 8)
+    F = max(1, min(F, args.steps))
+    nslot = max(1, args.frames_in_flight if args.frames_in_flight else (3 if F == 1 else 2))
     scenes = [_lib.DeviceScene(spheres, bg, local_rank) for _ in range(nslot)]
-    outs = [torch.empty((rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
+    outs = [torch.empty((F, rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslot - 1)]
     scene, out, stream = scenes[0], outs[0], streams[0]
 
-    def render(k=0, seg_ptr=None):
-        scenes[k].render_async(cam._state, params, outs[k].data_ptr(), seg_ptr, streams[k].cuda_stream)
+    def launch(k, first, n):
+        """Frames first .. first + n - 1 (progressive passes) in slot k."""
+        p = _lib.Params.from_buffer_copy(params)
+        p.pass_ = first % 4096
+        if n == 1:
+            scenes[k].render_async(cam._state, p, outs[k].data_ptr(), None, streams[k].cuda_stream)
+        else:
+            scenes[k].render_passes_async(cam._state, p, n, outs[k].data_ptr(), streams[k].cuda_stream)
 
-    def step(i):
-        k = i % nslot
-        with torch.cuda.stream(streams[k]):
-            render(k)
-            if world > 1:
-                shard.gather_image(outs[k], H, args.tile_rows, world, rank)
+    def frames(first, count):
+        j = 0
+        for i in range(first, first + count, F):
+            n = min(F, first + count - i)
+            k = j % nslot
+            with torch.cuda.stream(streams[k]):
+                launch(k, i, n)
+                if world > 1:
+                    shard.gather_frames(outs[k][:n], H, args.tile_rows, world, rank)
+            j += 1
 
     # Untimed instrumented launch: segments, ray-sphere and ray-box tests for the roofline.
-    stats = torch.zeros(3, dtype=torch.int64, device="cuda")
-    scene.render_stats_async(cam._state, params, out.data_ptr(), stats.data_ptr(), stream.cuda_stream)
-    torch.cuda.synchronize()
-    segments_local, sphere_tests, box_tests = (int(v) for v in stats.tolist())
+    # One per frame of the roofline's launch (passes 0 .. F-1).
+    segments_local = sphere_tests = box_tests = 0
+    for k in range(F):
+        stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+        p = _lib.Params.from_buffer_copy(params)
+        p.pass_ = k
+        scene.render_stats_async(cam._state, p, out.data_ptr(), stats.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        seg_k, sph_k, box_k = (int(v) for v in stats.tolist())
+        segments_local, sphere_tests, box_tests = segments_local + seg_k, sphere_tests + sph_k, box_tests + box_k
 
     for k in range(nslot):  # setup: each slot's sample buffer and launch state
-        render(k)
-    for i in range(args.warmup):
-        step(i)
+        launch(k, 0, F)
+    frames(0, args.warmup)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
+    frames(args.warmup, args.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # Untimed: one frame at a time, HIP events on the launch stream, for the
-    # roofline's per-launch duration.
+    # Untimed: one launch at a time, HIP events on the launch stream, for the
+    # roofline's per-launch duration (a launch renders F frames).
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
     for a, b in ev:
         a.record(stream)
-        render(0)
+        launch(0, 0, F)
         b.record(stream)
     torch.cuda.synchronize()
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -185,10 +220,13 @@ def main() -> int:
             "spheres": int(len(spheres)), "output": "float3 f32 linear", "parallelism": f"row-tiles x{world}",
             "tile_rows": args.tile_rows if world > 1 else 0,
             "frames_in_flight": nslot,
+            "frames_per_launch": F,
         },
     }
+    if world > 1 and backend != "nccl":
+        rec["rehearsal_backend"] = backend  # code-path check only, not a measurement
     if rank == 0:
-        local_samples = rows * W * spp
+        local_samples = rows * W * spp * F  # per launch: F frames
         ops64 = 17.0 * sphere_tests + 60.0 * segments_local + 40.0 * local_samples
         ops32 = 11.0 * box_tests
         ops = ops64 + 0.5 * ops32
@@ -199,7 +237,7 @@ def main() -> int:
         out_bytes = local_samples * 24 + len(spheres) * (32 + 64)
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-        if os.path.exists(pmc_path):
+        if os.path.exists(pmc_path) and world == 1 and F == 1:  # measured on that launch shape
             try:
                 traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
@@ -212,6 +250,7 @@ def main() -> int:
             "frac": round(achieved / FP64_PEAK_OPS, 4),
             "traffic": traffic,
             "kernel_ms": round(kernel_ms, 4),
+            "frames_per_launch": F,
             "segments_per_launch": segments_local,
             "sphere_tests_per_launch": sphere_tests,
             "box_tests_per_launch": box_tests,
@@ -231,7 +270,8 @@ def main() -> int:
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed,
                                                args.cpu_row_step)
-    print(json.dumps(rec), flush=True)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
     for sc in scenes:
         sc.release()
     if dist:

@@ -146,7 +146,9 @@ typedef struct tray_params {
     int32_t tile_index; /* 0 <= tile_index < tile_count */
     int32_t output;     /* tray_output */
     int32_t flags;      /* TRAY_FLAG_* */
-    int32_t reserved;   /* must be 0 */
+    int32_t pass;       /* progressive pass, >= 0: sample s of a pixel uses the counter RNG's sample
+                           word pass * rays_per_pixel + s, so passes 0, 1, ... are independent frames
+                           of the same pixels (0: the single frame of Tracer.Render) */
 } tray_params;
 
 /* Force the reference-order linear scan over all spheres (Scene.Hit,
@@ -216,6 +218,15 @@ int tray_scene_get_info(tray_scene_t scene, tray_scene_info *out);
  * params->output format; segments_device nullable. Returns after enqueueing. */
 int tray_render_async(tray_scene_t scene, const tray_camera *camera, const tray_params *params, void *out_device,
                       uint32_t *segments_device, void *stream);
+
+/* Consecutive progressive passes params->pass .. params->pass + n_passes - 1 of
+ * the row set, as ONE persistent launch (per band): a lane that finishes its
+ * last sample of pass k takes a sample of pass k + 1, so frames follow each
+ * other with no per-frame tail of long paths. Frame k (bit-identical to
+ * tray_render_async with pass = params->pass + k) is written at out_device +
+ * k * rows * width * bytes-per-pixel. No segments output. */
+int tray_render_passes_async(tray_scene_t scene, const tray_camera *camera, const tray_params *params,
+                             int32_t n_passes, void *out_device, void *stream);
 
 /* tray_render_async with instrumentation, for roofline accounting: writes the
  * frame as TRAY_OUT_RGB_F32 into out_device (params->output is ignored) and

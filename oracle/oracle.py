@@ -54,10 +54,10 @@ def lib() -> ctypes.CDLL:
         L = ctypes.CDLL(_LIB_PATH)
         L.oracle_render_rows.argtypes = [_vp, ctypes.c_int, _dp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_double, ctypes.c_uint64, _i32p, ctypes.c_int,
-                                         ctypes.c_int, _dp, _u32p]
+                                         ctypes.c_int, _dp, _u32p, ctypes.c_int]
         L.oracle_render_pixels.argtypes = [_vp, ctypes.c_int, _dp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_double, ctypes.c_uint64, _i32p, _i32p,
-                                           ctypes.c_int, _dp, _u32p]
+                                           ctypes.c_int, _dp, _u32p, ctypes.c_int]
         L.oracle_ray_color.argtypes = [_vp, ctypes.c_int, _dp, _dp, _dp, ctypes.c_int, ctypes.c_uint64,
                                        ctypes.c_uint32, ctypes.c_uint32, _dp, _u32p]
         L.oracle_philox4x32_10.argtypes = [_u32p, _u32p, _u32p]
@@ -250,7 +250,7 @@ DEFAULT_BACKGROUND = np.array([1.0, 1.0, 1.0, 0.4, 0.65, 1.0])  # ray/objects.go
 
 # ---------------------------------------------------------------- render ----
 def render_rows(spheres, background, camera, width, height, spp, max_depth, ray_radius, seed, rows,
-                workers=1, segments=True):
+                workers=1, segments=True, pass_=0):
     """Render a list of image rows -> (len(rows), W, 3) float64 [+ (len(rows), W) uint32 segments]."""
     s = _spheres(spheres)
     rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
@@ -258,20 +258,21 @@ def render_rows(spheres, background, camera, width, height, spp, max_depth, ray_
     seg = np.zeros((len(rows), width), dtype=np.uint32) if segments else None
     rc = lib().oracle_render_rows(s.ctypes.data, len(s), _d(_f64(background, 6)), _f64(camera, 21).ctypes.data,
                                   width, height, spp, max_depth, ray_radius, seed, rows.ctypes.data_as(_i32p),
-                                  len(rows), workers, _d(out), seg.ctypes.data_as(_u32p) if seg is not None else None)
+                                  len(rows), workers, _d(out), seg.ctypes.data_as(_u32p) if seg is not None else None,
+                                  int(pass_))
     if rc != 0:
         raise ValueError(f"oracle_render_rows failed: {rc}")
     return (out, seg) if segments else out
 
 
 def render(spheres, background, camera, width, height, spp, max_depth, ray_radius, seed, y_start=0, y_end=None,
-           workers=1, segments=True):
+           workers=1, segments=True, pass_=0):
     y_end = height if y_end is None else y_end
     return render_rows(spheres, background, camera, width, height, spp, max_depth, ray_radius, seed,
-                       np.arange(y_start, y_end, dtype=np.int32), workers, segments)
+                       np.arange(y_start, y_end, dtype=np.int32), workers, segments, pass_)
 
 
-def render_pixels(spheres, background, camera, width, height, spp, max_depth, ray_radius, seed, xs, ys):
+def render_pixels(spheres, background, camera, width, height, spp, max_depth, ray_radius, seed, xs, ys, pass_=0):
     s = _spheres(spheres)
     xs = np.ascontiguousarray(np.asarray(xs, dtype=np.int32))
     ys = np.ascontiguousarray(np.asarray(ys, dtype=np.int32))
@@ -279,7 +280,7 @@ def render_pixels(spheres, background, camera, width, height, spp, max_depth, ra
     seg = np.zeros(len(xs), dtype=np.uint32)
     rc = lib().oracle_render_pixels(s.ctypes.data, len(s), _d(_f64(background, 6)), _f64(camera, 21).ctypes.data,
                                     width, height, spp, max_depth, ray_radius, seed, xs.ctypes.data_as(_i32p),
-                                    ys.ctypes.data_as(_i32p), len(xs), _d(out), seg.ctypes.data_as(_u32p))
+                                    ys.ctypes.data_as(_i32p), len(xs), _d(out), seg.ctypes.data_as(_u32p), int(pass_))
     if rc != 0:
         raise ValueError(f"oracle_render_pixels failed: {rc}")
     return out, seg

@@ -424,6 +424,7 @@ typedef struct {
     int width, height, spp, max_depth;
     double ray_radius;
     uint64_t seed;
+    uint32_t sample_base; /* progressive pass x spp (tray_params.pass, include/tray.h) */
 } o_params;
 
 /* One pixel of Tracer.RenderLines ray/tracer.go:129-145 (linear mean colour). */
@@ -435,7 +436,7 @@ static int render_pixel(const scene *sc, const o_camera *cam, const o_params *p,
     uint32_t segs = 0;
     int err = 0;
     for (int s = 0; s < p->spp; ++s) {
-        rngkey k = {p->seed, (uint32_t)y * (uint32_t)p->width + (uint32_t)x, (uint32_t)s};
+        rngkey k = {p->seed, (uint32_t)y * (uint32_t)p->width + (uint32_t)x, p->sample_base + (uint32_t)s};
         double ox = 0.0, oy = 0.0;
         if (multiple_rays) in_disc(k, 0, p->ray_radius, &ox, &oy);
         ray r = get_ray(cam, k, (double)x, (double)y, ox, oy);
@@ -504,13 +505,14 @@ static int valid_scene(const o_sphere *sp, int n) {
 ORACLE_EXPORT int oracle_render_rows(const o_sphere *spheres, int n, const double bg[6], const o_camera *cam,
                                      int width, int height, int spp, int max_depth, double ray_radius,
                                      uint64_t seed, const int32_t *rows, int nrows, int workers, double *out_rgb,
-                                     uint32_t *out_segments) {
+                                     uint32_t *out_segments, int pass) {
     if (width <= 0 || height <= 0 || spp <= 0 || max_depth <= 0 || nrows < 0 || (n > 0 && !spheres)) return -1;
     if (!valid_scene(spheres, n)) return -2;
     for (int i = 0; i < nrows; ++i)
         if (rows[i] < 0 || rows[i] >= height) return -1;
     scene sc = {spheres, n, V(bg[0], bg[1], bg[2]), V(bg[3], bg[4], bg[5])};
-    o_params p = {width, height, spp, max_depth, ray_radius, seed};
+    if (pass < 0) return -1;
+    o_params p = {width, height, spp, max_depth, ray_radius, seed, (uint32_t)pass * (uint32_t)spp};
     job j = {&sc, cam, &p, rows, nrows, 0, out_rgb, out_segments, 0, 0};
     if (workers <= 1) {
         render_row_range(&j, 0, nrows);
@@ -529,11 +531,11 @@ ORACLE_EXPORT int oracle_render_rows(const o_sphere *spheres, int n, const doubl
 ORACLE_EXPORT int oracle_render_pixels(const o_sphere *spheres, int n, const double bg[6], const o_camera *cam,
                                        int width, int height, int spp, int max_depth, double ray_radius,
                                        uint64_t seed, const int32_t *xs, const int32_t *ys, int count,
-                                       double *out_rgb, uint32_t *out_segments) {
-    if (width <= 0 || height <= 0 || spp <= 0 || max_depth <= 0) return -1;
+                                       double *out_rgb, uint32_t *out_segments, int pass) {
+    if (width <= 0 || height <= 0 || spp <= 0 || max_depth <= 0 || pass < 0) return -1;
     if (!valid_scene(spheres, n)) return -2;
     scene sc = {spheres, n, V(bg[0], bg[1], bg[2]), V(bg[3], bg[4], bg[5])};
-    o_params p = {width, height, spp, max_depth, ray_radius, seed};
+    o_params p = {width, height, spp, max_depth, ray_radius, seed, (uint32_t)pass * (uint32_t)spp};
     for (int i = 0; i < count; ++i) {
         uint32_t s = 0;
         if (xs[i] < 0 || xs[i] >= width || ys[i] < 0 || ys[i] >= height) return -1;

@@ -350,3 +350,71 @@ def test_stack_overflow_area(L, O, monkeypatch):
     monkeypatch.setenv("TRAY_STACK_LDS_SLOTS", "8")
     b, sb = gpu_render(L, sc, DEFAULT_BG, st, 64, 36, 4, 50, 0.5, 3)
     assert np.array_equal(sa, sb) and np.array_equal(a, b)
+
+
+def test_progressive_pass_vs_oracle(L, O):
+    """tray_params.pass: sample s of a pixel draws RNG sample word pass*r + s
+    (include/tray.h). A later pass matches the oracle's render of that pass and
+    differs from pass 0."""
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, 64, 36)
+    rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, 64, 36, 4, 50, 0.5, 2, pass_=3)
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), 64, 36, 4, 50, 0.5, 2, workers=WORKERS, pass_=3)
+    check(rgb, seg, ref, rseg)
+    first, _ = gpu_render(L, sc, DEFAULT_BG, st, 64, 36, 4, 50, 0.5, 2)
+    assert not np.array_equal(first, rgb)
+
+
+def _passes(L, dev, st, p, n, dtype, shape):
+    import torch
+
+    out = torch.zeros((n,) + shape, dtype=dtype, device="cuda")
+    dev.render_passes_async(st, p, n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("bands", [False, True])
+def test_passes_launch_equals_single_passes(L, O, monkeypatch, bands):
+    """tray_render_passes_async: n progressive passes in one persistent launch
+    are bit-identical to n single-pass renders, in every output format, with one
+    or several launch bands and with row tiles."""
+    import torch
+
+    sc = O.rich_scene(2)
+    w, h, spp = 72, 41, 3
+    st = camera(L, RICH_SETUP, w, h)
+    if bands:
+        monkeypatch.setenv("TRAY_BAND_SAMPLES", str(72 * 8 * 3 * 3 * 2))  # two 8-row tile rows per band
+    dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
+    try:
+        for fmt, dtype, ch in [(L.OUT_RGB_F64, torch.float64, 3), (L.OUT_RGB_F32, torch.float32, 3),
+                               (L.OUT_RGBA8, torch.uint8, 4)]:
+            for tiles in [{}, dict(tile_rows=4, tile_count=3, tile_index=2)]:
+                p = L.make_params(w, h, 20, spp, 0.5, 9, output=fmt, pass_=2, **tiles)
+                rows = L.params_rows(p)
+                frames = _passes(L, dev, st, p, 3, dtype, (rows, w, ch))
+                for k in range(3):
+                    q = L.make_params(w, h, 20, spp, 0.5, 9, output=fmt, pass_=2 + k, **tiles)
+                    one, _ = L.render(sc, bg_struct(L, DEFAULT_BG), st, q, 0)
+                    assert np.array_equal(frames[k], one), (fmt, tiles, k)
+                assert not np.array_equal(frames[0], frames[1])
+    finally:
+        dev.release()
+
+
+def test_passes_argument_checks(L, O):
+    import torch
+
+    dev = L.DeviceScene(O.rich_scene(2), bg_struct(L, DEFAULT_BG), 0)
+    st = camera(L, RICH_SETUP, 16, 8)
+    out = torch.zeros((2, 8, 16, 3), dtype=torch.float64, device="cuda")
+    try:
+        with pytest.raises(L.TrayError):
+            dev.render_passes_async(st, L.make_params(16, 8, 5, 4, 0.5, 1), 0, out.data_ptr())
+        with pytest.raises(L.TrayError):
+            dev.render_passes_async(st, L.make_params(16, 8, 5, 4, 0.5, 1, pass_=-1), 1, out.data_ptr())
+        with pytest.raises(L.TrayError):  # (pass + n) x r beyond the 32-bit sample word
+            dev.render_passes_async(st, L.make_params(16, 8, 5, 1 << 30, 0.5, 1, pass_=3), 2, out.data_ptr())
+    finally:
+        dev.release()

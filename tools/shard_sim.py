@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--frames-in-flight", type=int, default=1,
                     help="> 1: time --reps consecutive frames per shard overlapped this deep (bench.py's default is 3)")
+    ap.add_argument("--passes", type=int, default=1,
+                    help="frames per launch (tray_render_passes_async); times are per frame")
     ap.add_argument("--lib", default=None, help="a libtray_amd.so build to load (default: the in-tree one)")
     args = ap.parse_args()
     import numpy as np
@@ -46,12 +48,20 @@ def main():
              for _ in range(nslot - 1)]
     streams = [torch.cuda.Stream() for _ in range(nslot)]
 
+    F = max(1, args.passes)
+
+    def launch(sc, p, out, stream):
+        if F == 1:
+            sc.render_async(cam._state, p, out.data_ptr(), None, stream.cuda_stream)
+        else:
+            sc.render_passes_async(cam._state, p, F, out.data_ptr(), stream.cuda_stream)
+
     def time_pipelined(n, k):
         p = shard.shard_params(base, args.tile_rows, n, k)
-        outs = [torch.empty((_lib.params_rows(p), W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
+        outs = [torch.empty((F, _lib.params_rows(p), W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
         scs = [scene] + extra
         for i in range(nslot):  # warm
-            scs[i].render_async(cam._state, p, outs[i].data_ptr(), None, streams[i].cuda_stream)
+            launch(scs[i], p, outs[i], streams[i])
         torch.cuda.synchronize()
         reps = max(args.reps, 4 * nslot)
         a = torch.cuda.Event(enable_timing=True)
@@ -60,17 +70,17 @@ def main():
             s_.wait_event(a)
         for i in range(reps):
             j = i % nslot
-            scs[j].render_async(cam._state, p, outs[j].data_ptr(), None, streams[j].cuda_stream)
+            launch(scs[j], p, outs[j], streams[j])
         ends = []
         for s_ in streams:
             e = torch.cuda.Event(enable_timing=True)
             e.record(s_)
             ends.append(e)
         torch.cuda.synchronize()
-        return max(a.elapsed_time(e) for e in ends) / reps
+        return max(a.elapsed_time(e) for e in ends) / (reps * F)
 
     def time_shard(n, k):
-        if nslot > 1:
+        if nslot > 1 or F > 1:
             return time_pipelined(n, k)
         p = shard.shard_params(base, args.tile_rows, n, k)
         out = torch.empty((_lib.params_rows(p), W, 3), dtype=torch.float32, device="cuda")
@@ -90,7 +100,7 @@ def main():
         times = [time_shard(n, k) for k in range(n)]
         if n == 1:
             t1 = times[0]
-        rec = {"config": args.config, "n": n, "tile_rows": args.tile_rows, "frames_in_flight": nslot, "max_ms": round(max(times), 4),
+        rec = {"config": args.config, "n": n, "tile_rows": args.tile_rows, "frames_in_flight": nslot, "passes": F, "max_ms": round(max(times), 4),
                "min_ms": round(min(times), 4), "mean_ms": round(float(np.mean(times)), 4)}
         if t1:
             rec["render_efficiency"] = round(t1 / (n * max(times)), 4)

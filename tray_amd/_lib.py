@@ -93,7 +93,7 @@ class Params(ctypes.Structure):
         ("tile_index", ctypes.c_int32),
         ("output", ctypes.c_int32),
         ("flags", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("pass_", ctypes.c_int32),  # tray_params.pass (progressive pass)
     ]
 
 
@@ -130,6 +130,7 @@ EXPORTS = (
     "tray_scene_release",
     "tray_scene_get_info",
     "tray_render_async",
+    "tray_render_passes_async",
     "tray_render_stats_async",
     "tray_params_rows",
     "tray_to_srgba",
@@ -169,6 +170,8 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.tray_scene_get_info.argtypes = [vp, ctypes.POINTER(SceneInfo)]
     L.tray_render_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
     L.tray_render_stats_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
+    if hasattr(L, "tray_render_passes_async"):  # absent from older builds (A/B tools)
+        L.tray_render_passes_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), i32, vp, vp]
     L.tray_params_rows.argtypes = [ctypes.POINTER(Params)]
     L.tray_params_rows.restype = i32
     L.tray_to_srgba.argtypes = [vp, ctypes.c_size_t, vp]
@@ -196,9 +199,9 @@ def spheres_array(spheres) -> np.ndarray:
 
 
 def make_params(width, height, max_depth, rays_per_pixel, ray_radius, seed, y_start=0, y_end=None,
-                tile_rows=0, tile_count=1, tile_index=0, output=OUT_RGB_F64, flags=0) -> Params:
+                tile_rows=0, tile_count=1, tile_index=0, output=OUT_RGB_F64, flags=0, pass_=0) -> Params:
     return Params(width, height, max_depth, rays_per_pixel, float(ray_radius), int(seed) & (2**64 - 1), y_start,
-                  height if y_end is None else y_end, tile_rows, tile_count, tile_index, output, flags, 0)
+                  height if y_end is None else y_end, tile_rows, tile_count, tile_index, output, flags, pass_)
 
 
 def params_rows(p: Params) -> int:
@@ -243,6 +246,15 @@ class DeviceScene:
                      stream: int | None = None) -> None:
         rc = self.L.tray_render_async(self.handle, ctypes.byref(camera), ctypes.byref(params), out_ptr, segments_ptr,
                                       stream)
+        if rc != TRAY_OK:
+            raise TrayError(rc, self.L.tray_last_error().decode())
+
+    def render_passes_async(self, camera: CameraState, params: Params, n_passes: int, out_ptr: int,
+                            stream: int | None = None) -> None:
+        """Progressive passes params.pass_ .. + n_passes - 1 in one persistent launch;
+        frame k at out_ptr + k * rows * width * bytes-per-pixel."""
+        rc = self.L.tray_render_passes_async(self.handle, ctypes.byref(camera), ctypes.byref(params), int(n_passes),
+                                             out_ptr, stream)
         if rc != TRAY_OK:
             raise TrayError(rc, self.L.tray_last_error().decode())
 

@@ -145,6 +145,9 @@ static int validate_params(const tray_params* p) {
     if (p->output < TRAY_OUT_RGB_F64 || p->output > TRAY_OUT_RGBA8)
         return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown output format");
     if (p->flags & ~TRAY_FLAG_LINEAR_SCAN) return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown flags");
+    if (p->pass < 0) return fail(TRAY_ERR_INVALID_ARGUMENT, "pass must be >= 0");
+    if ((uint64_t)(p->pass + 1) * (uint64_t)p->rays_per_pixel > 0x100000000ull)
+        return fail(TRAY_ERR_TOO_LARGE, "pass x rays_per_pixel exceeds the 32-bit RNG sample word");
     return TRAY_OK;
 }
 
@@ -351,10 +354,14 @@ int tray_scene_release(tray_scene_t sc) {
 }
 
 static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
-                             uint32_t* segments_device, unsigned long long* stats_device, void* stream) {
+                             uint32_t* segments_device, unsigned long long* stats_device, void* stream,
+                             int32_t n_passes = 1) {
     if (!sc || !cam || !out_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     int rc = validate_params(p);
     if (rc) return rc;
+    if (n_passes < 1) return fail(TRAY_ERR_INVALID_ARGUMENT, "n_passes must be >= 1");
+    if ((uint64_t)(p->pass + n_passes) * (uint64_t)p->rays_per_pixel > 0x100000000ull)
+        return fail(TRAY_ERR_TOO_LARGE, "(pass + n_passes) x rays_per_pixel exceeds the 32-bit RNG sample word");
     KernelParams k;
     memset(&k, 0, sizeof(k));
     k.geo = sc->geo;
@@ -385,6 +392,9 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.bg_a = sc->bg_a;
     k.bg_b = sc->bg_b;
     k.out = out_device;
+    k.passes = (uint32_t)n_passes;
+    k.pass0 = (uint32_t)p->pass;
+    k.out_frame_bytes = (size_t)k.rows * (size_t)p->width * bytes_per_pixel(p->output);
     k.segments = segments_device;
     k.stats = stats_device;
     k.nodes = sc->nodes;
@@ -407,9 +417,10 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
                   std::fabs(cam->defocus_v[0]) + std::fabs(cam->defocus_v[1]) + std::fabs(cam->defocus_v[2]);
     const bool use_bvh = sc->has_bvh && !(p->flags & TRAY_FLAG_LINEAR_SCAN) && cam_extent <= sc->bvh_bound;
     TRAY_HIP(hipSetDevice(sc->device));
-    if (!band_fits(p->width, p->rays_per_pixel))
-        return fail(TRAY_ERR_TOO_LARGE, "width x rays_per_pixel too large (8 rows of samples exceed 2^31)");
-    const size_t need = sample_buffer_bytes(p->width, k.rows, p->rays_per_pixel);
+    const uint64_t spp_launch = (uint64_t)p->rays_per_pixel * (uint64_t)n_passes;
+    if (!band_fits(p->width, spp_launch))
+        return fail(TRAY_ERR_TOO_LARGE, "width x rays_per_pixel x passes too large (8 rows of samples exceed 2^31)");
+    const size_t need = sample_buffer_bytes(p->width, k.rows, spp_launch);
     if (need > sc->samples_bytes) {
         if (sc->samples) {
             TRAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
@@ -428,6 +439,11 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
 int tray_render_async(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
                       uint32_t* segments_device, void* stream) {
     return render_async_impl(sc, cam, p, out_device, segments_device, nullptr, stream);
+}
+
+int tray_render_passes_async(tray_scene_t sc, const tray_camera* cam, const tray_params* p, int32_t n_passes,
+                             void* out_device, void* stream) {
+    return render_async_impl(sc, cam, p, out_device, nullptr, nullptr, stream, n_passes);
 }
 
 int tray_render_stats_async(tray_scene_t sc, const tray_camera* cam, const tray_params* p, float* out_device,

@@ -674,7 +674,17 @@ __device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t d, double rinv, ui
     return (uint32_t)q;
 }
 
-__device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, int32_t& x, int32_t& j, uint32_t& s) {
+// With several progressive passes in the launch, item i is item i % frame_items
+// of pass i / frame_items (a 64-item chunk never straddles two passes:
+// frame_items is a multiple of 64). `k` returns the pass within the launch.
+__device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, int32_t& x, int32_t& j, uint32_t& s,
+                                            uint32_t& k) {
+    k = 0;
+    if (p.passes > 1) {
+        uint32_t li;
+        k = udiv(i, p.frame_items, p.inv_frame_items, li);
+        i = li;
+    }
     const uint32_t q = udiv(i, (uint32_t)p.spp, p.inv_spp, s);
     const uint32_t tile = q >> 6, r = q & 63u;
     uint32_t tx;
@@ -693,7 +703,7 @@ __device__ __forceinline__ void start_sample(const KernelParams& p, UniPtr uni, 
     L.x = x;
     L.j = j;
     L.pixel = (uint32_t)y * (uint32_t)p.width + (uint32_t)x;  // global index: tiling-independent RNG key
-    L.sample = s;
+    L.sample = s;  // the RNG sample word: pass * spp + sample
     L.bounce = 0;
     L.segments = 0;
     L.thr = d3(1, 1, 1);
@@ -960,9 +970,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #endif
         if (fresh_item != ~0u) {
             int32_t x, j;
-            uint32_t smp;
-            if (fresh_item < p.items && decode_item(p, fresh_item, x, j, smp)) {
-                start_sample(p, uni, L, fresh_item, x, j, smp);
+            uint32_t smp, pass;
+            if (fresh_item < p.items && decode_item(p, fresh_item, x, j, smp, pass)) {
+                start_sample(p, uni, L, fresh_item, x, j, (p.pass0 + pass) * (uint32_t)p.spp + smp);
                 if constexpr (kBVH) {
                     ++L.segments;
                     trav_begin(T, sv, L.org, L.dir);
@@ -1068,15 +1078,17 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 // It also re-zeroes the work queue for the next band or launch on the stream
 // (the megakernel has finished with it), so no memset launch sits between
 // consecutive frames.
+// blockIdx.y is the pass within the launch.
 template <int kFmt>
 __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q == 0) *p.queue = 0u;
-    if (q >= p.items / (uint32_t)p.spp) return;
+    if (q == 0 && blockIdx.y == 0) *p.queue = 0u;
+    if (q >= p.frame_items / (uint32_t)p.spp) return;
+    const uint32_t item0 = blockIdx.y * p.frame_items + q * (uint32_t)p.spp;
     int32_t x, j;
-    uint32_t s0;
-    if (!decode_item(p, q * (uint32_t)p.spp, x, j, s0)) return;
-    const double* smp = p.samples + (size_t)q * (size_t)p.spp * 3;
+    uint32_t s0, pass;
+    if (!decode_item(p, item0, x, j, s0, pass)) return;
+    const double* smp = p.samples + (size_t)item0 * 3;
     D3 sum = d3(0, 0, 0);
     // Loads of 8 samples are issued together; the adds stay in sample order.
     int32_t s = 0;
@@ -1091,20 +1103,21 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
     const double inv = 1.0 / (double)p.spp;  // colorSumDiv (ray/tracer.go:123)
     const D3 mean = smul(sum, inv);
     const size_t off = (size_t)j * (size_t)p.width + (size_t)x;
+    void* const out = static_cast<char*>(p.out) + (size_t)pass * p.out_frame_bytes;
     if constexpr (kFmt == kOutRGBF64) {
-        double* o = static_cast<double*>(p.out) + off * 3;
+        double* o = static_cast<double*>(out) + off * 3;
         o[0] = mean.x;
         o[1] = mean.y;
         o[2] = mean.z;
     } else if constexpr (kFmt == kOutRGBF32) {
-        float* o = static_cast<float*>(p.out) + off * 3;
+        float* o = static_cast<float*>(out) + off * 3;
         o[0] = (float)mean.x;
         o[1] = (float)mean.y;
         o[2] = (float)mean.z;
     } else {
         const uint32_t rgba = linear_to_srgb(mean.x) | (linear_to_srgb(mean.y) << 8) |
                               (linear_to_srgb(mean.z) << 16) | (255u << 24);
-        static_cast<uint32_t*>(p.out)[off] = rgba;
+        static_cast<uint32_t*>(out)[off] = rgba;
     }
 }
 
@@ -1170,25 +1183,30 @@ uint64_t max_band_samples() {
     return kMaxBandSamples;
 }
 
-// Bands of 8-row tile rows, each <= max_band_samples() samples (at least one tile row).
-static int32_t band_tile_rows(int32_t width, int32_t spp) {
-    const uint64_t per = (uint64_t)((width + 7) / 8) * 64u * (uint64_t)spp;
+// Bands of 8-row tile rows, each <= max_band_samples() samples over all of the
+// launch's passes (at least one tile row). `spp` below counts the samples of a
+// pixel in one launch: rays_per_pixel x passes.
+static int32_t band_tile_rows(int32_t width, uint64_t spp) {
+    const uint64_t per = (uint64_t)((width + 7) / 8) * 64u * spp;
     return (int32_t)std::max<uint64_t>(1, max_band_samples() / per);
 }
 
-size_t sample_buffer_bytes(int32_t width, int32_t rows, int32_t spp) {
+size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp) {
     if (rows <= 0) return 0;
     const int32_t tile_rows = std::min(band_tile_rows(width, spp), (rows + 7) / 8);
     return (size_t)((width + 7) / 8) * 64u * (size_t)tile_rows * (size_t)spp * 3 * sizeof(double);
 }
 
-bool band_fits(int32_t width, int32_t spp) {
-    return (uint64_t)((width + 7) / 8) * 64u * (uint64_t)spp <= 0x7FFFFFFFull;
+bool band_fits(int32_t width, uint64_t spp) {
+    return (uint64_t)((width + 7) / 8) * 64u * spp <= 0x7FFFFFFFull;
 }
 
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (p.rows <= 0) return hipSuccess;
-    if (!band_fits(p.width, p.spp)) return hipErrorInvalidValue;
+    if (p.passes < 1) p.passes = 1;
+    const uint64_t spp_launch = (uint64_t)p.spp * p.passes;
+    if (!band_fits(p.width, spp_launch)) return hipErrorInvalidValue;
+    if (p.segments && p.passes > 1) return hipErrorInvalidValue;
     p.tiles_x = (p.width + 7) / 8;
     p.inv_spp = 1.0 / (double)p.spp;
     p.inv_tiles_x = 1.0 / (double)p.tiles_x;
@@ -1249,13 +1267,15 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         e = hipMemsetAsync(p.segments, 0, (size_t)p.rows * (size_t)p.width * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
-    const int32_t band = band_tile_rows(p.width, p.spp) * 8;
+    const int32_t band = band_tile_rows(p.width, spp_launch) * 8;
     const uint32_t waves = (uint32_t)threads / 64u;
     for (int32_t j0 = 0; j0 < p.rows; j0 += band) {
         p.j0 = j0;
         p.band_rows = std::min(band, p.rows - j0);
         const uint32_t pixels = (uint32_t)p.tiles_x * (uint32_t)((p.band_rows + 7) / 8) * 64u;
-        p.items = pixels * (uint32_t)p.spp;
+        p.frame_items = pixels * (uint32_t)p.spp;
+        p.inv_frame_items = 1.0 / (double)p.frame_items;
+        p.items = p.frame_items * p.passes;
         p.nchunks = (p.items + 63u) / 64u;
         // Enough waves for every chunk, capped at what the device keeps resident.
         const uint32_t grid = std::min<uint32_t>((p.nchunks + waves - 1u) / waves, (uint32_t)blocks);
@@ -1263,7 +1283,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         hipLaunchKernelGGL(fn, dim3(grid), dim3(threads), lds, stream, p);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(resolve, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(resolve, dim3((pixels + 255u) / 256u, p.passes), dim3(256), 0, stream, p);
         e = hipGetLastError();
         if (e != hipSuccess) {
             (void)hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);  // keep the invariant

@@ -65,7 +65,11 @@ struct KernelParams {
     int32_t n_pad;       // round_up(n, 4) + 4
     int32_t tiles_x;     // 8x8 pixel tiles per compact row band
     uint32_t nchunks;    // 64-item chunks of the band's work items (one item = one sample)
-    uint32_t items;      // band work items: 8x8-tile-padded pixels x spp
+    uint32_t items;      // band work items: passes x frame_items
+    uint32_t frame_items;  // one pass's items of the band: 8x8-tile-padded pixels x spp
+    uint32_t passes, pass0;  // progressive passes pass0 .. pass0 + passes - 1 in this launch
+    double inv_frame_items;  // RN(1/frame_items)
+    size_t out_frame_bytes;  // output stride between passes
     int32_t j0, band_rows;  // the band: compact rows [j0, j0 + band_rows)
     double inv_spp, inv_tiles_x;  // RN(1/spp), RN(1/tiles_x): item decoding
     double* samples;     // per-item path colours (3 doubles), summed in order by the resolve kernel
@@ -97,12 +101,12 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
 
 // Samples per launch band (the sample buffer holds one band: 24 B per sample);
 // the TRAY_BAND_SAMPLES environment variable lowers it (tests exercise bands).
-constexpr uint64_t kMaxBandSamples = 1ull << 26;
+constexpr uint64_t kMaxBandSamples = 1ull << 28;  // 6.4 GB of sample buffer
 uint64_t max_band_samples();
 // Bytes of sample buffer launch_render needs for `rows` compact rows.
-size_t sample_buffer_bytes(int32_t width, int32_t rows, int32_t spp);
+size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp);
 // False when one 8-row band has more than 2^31 samples (item indices are 32-bit).
-bool band_fits(int32_t width, int32_t spp);
+bool band_fits(int32_t width, uint64_t spp);
 
 // LDS the BVH kernel needs to hold the whole BVH scene (plus its traversal
 // stacks) on chip; above kMaxLDSBytes it reads the scene from global memory.

@@ -39,22 +39,34 @@ def gather_image(local, height: int, tile_rows: int, world: int, rank: int, dst:
     return the assembled [height, W, C] image there (None elsewhere).
 
     Uses ONE torch.distributed.gather of equal-size (padded) buffers."""
+    full = gather_frames(local.unsqueeze(0), height, tile_rows, world, rank, dst, group)
+    return None if full is None else full[0]
+
+
+def gather_frames(local, height: int, tile_rows: int, world: int, rank: int, dst: int = 0, group=None):
+    """gather_image for a batch of frames (the passes of one
+    tray_render_passes_async launch): local [n, rows_r, W, C] -> [n, height, W, C]
+    on `dst`, with ONE gather for the whole batch (fewer, larger transfers over
+    xGMI)."""
     import torch
     import torch.distributed as dist
 
     counts = [len(rows_for(height, tile_rows, world, r)) for r in range(world)]
     max_rows = max(counts)
     pad = local
-    if local.shape[0] < max_rows:
-        pad = torch.zeros((max_rows,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-        pad[: local.shape[0]] = local
+    if local.shape[1] < max_rows:
+        pad = torch.zeros((local.shape[0], max_rows) + tuple(local.shape[2:]), dtype=local.dtype,
+                          device=local.device)
+        pad[:, : local.shape[1]] = local
+    elif not local.is_contiguous():
+        pad = local.contiguous()
     bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
     dist.gather(pad, gather_list=bufs, dst=dst, group=group)
     if rank != dst:
         return None
-    full = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    full = torch.empty((local.shape[0], height) + tuple(local.shape[2:]), dtype=local.dtype, device=local.device)
     for r in range(world):
-        full.index_copy_(0, _row_index(height, tile_rows, world, r, local.device), bufs[r][: counts[r]])
+        full.index_copy_(1, _row_index(height, tile_rows, world, r, local.device), bufs[r][:, : counts[r]])
     return full
 
 
