@@ -485,39 +485,7 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t be
 // One node visit: test the four child boxes, visit the nearest hit child next
 // (an inner node or a leaf) and push the other hit children far-to-near.
 // Returns the new lane state.
-#ifdef TRAY_NODE_ASM
-typedef float F4v __attribute__((ext_vector_type(4)));
-// The seven 16-B node reads of an LDS-resident node issued back to back, then
-// one wait (the compiler otherwise serialised the first three behind
-// lgkmcnt(0) waits). Early-clobber outputs: a read's destination must not
-// overlap an address another in-flight read still has to use.
-__device__ __forceinline__ void node_reads_lds(uint32_t base, uint32_t onx, uint32_t ofx, uint32_t ony, uint32_t ofy,
-                                               uint32_t onz, uint32_t ofz, float4& nx, float4& fx, float4& ny,
-                                               float4& fy, float4& nz, float4& fz, uint4& rf) {
-    F4v a, b, c, d, e, f, r;
-    asm volatile(
-        "ds_read_b128 %0, %7\n"
-        "ds_read_b128 %1, %8\n"
-        "ds_read_b128 %2, %9\n"
-        "ds_read_b128 %3, %10\n"
-        "ds_read_b128 %4, %11\n"
-        "ds_read_b128 %5, %12\n"
-        "ds_read_b128 %6, %13 offset:96\n"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d), "=&v"(e), "=&v"(f), "=&v"(r)
-        : "v"(base + onx), "v"(base + ofx), "v"(base + ony), "v"(base + ofy), "v"(base + onz), "v"(base + ofz),
-          "v"(base));
-    nx = make_float4(a.x, a.y, a.z, a.w);
-    fx = make_float4(b.x, b.y, b.z, b.w);
-    ny = make_float4(c.x, c.y, c.z, c.w);
-    fy = make_float4(d.x, d.y, d.z, d.w);
-    nz = make_float4(e.x, e.y, e.z, e.w);
-    fz = make_float4(f.x, f.y, f.z, f.w);
-    rf = make_uint4(__float_as_uint(r.x), __float_as_uint(r.y), __float_as_uint(r.z), __float_as_uint(r.w));
-}
-#endif
-
-template <bool kLdsNodes, class Stk>
+template <class Stk>
 __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, const Stk& S, uint32_t& tested) {
     constexpr int32_t kPlane = 4 * kBvhWidth;  // far plane block = near ^ kPlane
     const char* nb = reinterpret_cast<const char*>(sv.nodes + T.cur);
@@ -529,25 +497,13 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
     tested = 0;
 #pragma unroll
     for (int g = 0; g < kBvhWidth / 4; ++g) {  // four children per group of 16-B loads
-        float4 nx, fx, ny, fy, nz, fz;
-        uint4 rf;
-#ifdef TRAY_NODE_ASM
-        if constexpr (kLdsNodes && kBvhWidth == 4) {
-            const uint32_t base =
-                (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(nb);
-            node_reads_lds(base, T.near_x, T.near_x ^ kPlane, T.near_y, T.near_y ^ kPlane, T.near_z,
-                           T.near_z ^ kPlane, nx, fx, ny, fy, nz, fz, rf);
-        } else
-#endif
-        {
-            nx = *reinterpret_cast<const float4*>(nb + T.near_x + 16 * g);
-            fx = *reinterpret_cast<const float4*>(nb + (T.near_x ^ kPlane) + 16 * g);
-            ny = *reinterpret_cast<const float4*>(nb + T.near_y + 16 * g);
-            fy = *reinterpret_cast<const float4*>(nb + (T.near_y ^ kPlane) + 16 * g);
-            nz = *reinterpret_cast<const float4*>(nb + T.near_z + 16 * g);
-            fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ kPlane) + 16 * g);
-            rf = *reinterpret_cast<const uint4*>(nb + 6 * kPlane + 16 * g);
-        }
+        const float4 nx = *reinterpret_cast<const float4*>(nb + T.near_x + 16 * g);
+        const float4 fx = *reinterpret_cast<const float4*>(nb + (T.near_x ^ kPlane) + 16 * g);
+        const float4 ny = *reinterpret_cast<const float4*>(nb + T.near_y + 16 * g);
+        const float4 fy = *reinterpret_cast<const float4*>(nb + (T.near_y ^ kPlane) + 16 * g);
+        const float4 nz = *reinterpret_cast<const float4*>(nb + T.near_z + 16 * g);
+        const float4 fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ kPlane) + 16 * g);
+        const uint4 rf = *reinterpret_cast<const uint4*>(nb + 6 * kPlane + 16 * g);
         const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
         const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
         const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
@@ -1009,7 +965,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     PROF_CNT(12, __popcll(__ballot(state == kShadeState)));  // waiting for the shade phase
                     if (state == kTravState) {
                         uint32_t tested;
-                        state = trav_node<kLDS>(T, sv, S, tested);
+                        state = trav_node(T, sv, S, tested);
                         if constexpr (kStats) st.boxes += tested;
                     }
                 }
