@@ -264,6 +264,7 @@ def main() -> int:
                                   "note": "reference work (every sphere tested per segment) / measured time"},
             "traversal": "linear scan" if args.linear else "exact-culling 4-wide BVH",
             "hbm": {"achieved_GBs": round(out_bytes / (kernel_ms * 1e-3) / 1e9, 3), "peak_GBs": HBM_PEAK_GBS,
+                    "frac": round(out_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                     "algorithmic_bytes_per_launch": out_bytes,
                     "note": "not the bound; megakernel only (traffic: profiles/pmc_<config>.json)"},
         }
