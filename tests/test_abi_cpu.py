@@ -108,7 +108,7 @@ def _render_rc(L, spheres=None, **kw):
     "kw",
     [dict(width=0), dict(height=-1), dict(max_depth=0), dict(rays_per_pixel=0), dict(ray_radius=float("inf")),
      dict(y_start=5, y_end=3), dict(y_end=9), dict(tile_rows=4, tile_count=2, tile_index=2), dict(tile_rows=-1),
-     dict(output=7)],
+     dict(output=7), dict(pass_=-1)],
 )
 def test_invalid_params_rejected_before_device(L, kw):
     assert _render_rc(L, **kw) == L.TRAY_ERR_INVALID_ARGUMENT
@@ -120,6 +120,12 @@ def test_unsupported_material(L):
     s["material"] = [1, 9]
     assert _render_rc(L, s) == L.TRAY_ERR_UNSUPPORTED
     assert b"unsupported material" in L.lib().tray_last_error()
+
+
+def test_pass_beyond_rng_sample_word(L):
+    # tray_params.pass: (pass + 1) x rays_per_pixel must fit the 32-bit RNG sample word
+    assert _render_rc(L, rays_per_pixel=1 << 20, pass_=4096) == L.TRAY_ERR_TOO_LARGE
+    assert b"sample word" in L.lib().tray_last_error()
 
 
 def test_too_many_pixels(L):
