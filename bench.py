@@ -17,9 +17,9 @@ draws fresh samples). --passes F renders F frames per launch
 so a launch has one tail of long paths, not F; default 1 at N = 1, 8 at N > 1,
 where a shard is ~1 ms of work and a d=50 tail would cost ~10 %), with ONE
 gather per launch. Launches rotate over --frames-in-flight slots (own device
-scene - work queue, sample buffer -, output and stream; default 3 at F = 1,
-else 2), so a launch's workgroups start on the CUs the previous launch's last
-long paths leave idle. Every step still renders its whole frame inside the
+scene - work queue, sample buffer -, output and stream; default 3), so a
+launch's workgroups start on the CUs the previous launch's last long paths
+leave idle. Every step still renders its whole frame inside the
 timed region.
 
 Also reported (rank 0):
@@ -83,8 +83,7 @@ def main() -> int:
     ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")
     ap.add_argument("--frames-in-flight", type=int, default=None,
                     help="launches overlap this deep (own scene copy, output and stream each): a launch's "
-                         "blocks start on CUs the previous launch's last paths leave idle "
-                         "(default 3 with one frame per launch, else 2)")
+                         "blocks start on CUs the previous launch's last paths leave idle (default 3)")
     ap.add_argument("--passes", type=int, default=None,
                     help="frames per launch (tray_render_passes_async: consecutive progressive passes, one "
                          "persistent launch, no per-frame tail); default 1 at N = 1, 8 at N > 1")
@@ -131,7 +130,7 @@ def main() -> int:
     # last paths leave idle. A small shard (N > 1) is dominated by those tails.
     F = args.passes if args.passes else (1 if world == 1 else 8)
     F = max(1, min(F, args.steps))
-    nslot = max(1, args.frames_in_flight if args.frames_in_flight else (3 if F == 1 else 2))
+    nslot = max(1, args.frames_in_flight if args.frames_in_flight else 3)
     scenes = [_lib.DeviceScene(spheres, bg, local_rank) for _ in range(nslot)]
     outs = [torch.empty((F, rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslot - 1)]
