@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtray_amd.so")
+# TRAY_LIB points the binding at another build of the same ABI (A/B tooling only).
+LIB_PATH = os.environ.get("TRAY_LIB") or os.path.join(_HERE, "libtray_amd.so")
 
 # include/tray.h enums
 TRAY_OK = 0
