@@ -135,6 +135,7 @@ struct Uniforms {
     double focus_time, ray_radius;
     uint64_t seed;
     uint64_t pool;  // the workgroup's chunk pool: (end << 32) | next (take_chunk)
+    uint32_t pool_chunks;  // chunks per pool refill (read only when refilling)
 };
 // Explicit LDS address space: a generic volatile pointer would be accessed with
 // (slow, system-coherent) flat loads.
@@ -578,7 +579,11 @@ __device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, cons
 // device-scope atomic round trip) the workgroup's other hungry waves sleep:
 // 16 -> 64 chunks cut C2 another 2-3 % (48-128 are within noise, 256 loses).
 // Waves take single chunks from their workgroup's pool in LDS, so the end of
-// the frame stays balanced at one chunk per wave.
+// the frame stays balanced at one chunk per wave. Small launches get smaller
+// pools (launch_render: every workgroup refills >= 8 times on average, pools
+// of 16..TRAY_POOL_CHUNKS chunks): with 64-chunk pools a 400x225 r=16 frame
+// (22.5 K chunks) hands the first 256 workgroups 64 chunks each and leaves
+// the rest to a few.
 #ifndef TRAY_POOL_CHUNKS
 #define TRAY_POOL_CHUNKS 64
 #endif
@@ -602,11 +607,12 @@ __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni
         if (next < end) return next;
         if (next == end) {  // first past the end: refill
             uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(p.queue, (uint32_t)TRAY_POOL_CHUNKS);
+            const uint32_t pool_chunks = __builtin_amdgcn_readfirstlane(uni->pool_chunks);
+            if (lane == 0) base = atomicAdd(p.queue, pool_chunks);
             base = __builtin_amdgcn_readlane(base, 0);
             const uint64_t fresh = base >= p.nchunks
                                        ? (uint64_t)kPoolDone << 32
-                                       : ((uint64_t)min(base + (uint32_t)TRAY_POOL_CHUNKS, p.nchunks) << 32) | base;
+                                       : ((uint64_t)min(base + pool_chunks, p.nchunks) << 32) | base;
             if (lane == 0) __hip_atomic_store(pool, fresh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             continue;
         }
@@ -838,6 +844,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         u->ray_radius = p.ray_radius;
         u->seed = p.seed;
         u->pool = 0;  // empty: the first taker refills it
+        u->pool_chunks = p.pool_chunks;
     }
     const UniPtr uni = uni_lds;
     SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single != 0,       p.bgeo, p.bidx,
@@ -1236,6 +1243,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         p.inv_frame_items = 1.0 / (double)p.frame_items;
         p.items = p.frame_items * p.passes;
         p.nchunks = (p.items + 63u) / 64u;
+        p.pool_chunks = std::min<uint32_t>(TRAY_POOL_CHUNKS, std::max<uint32_t>(16u, p.nchunks / (8u * (uint32_t)blocks)));
         // Enough waves for every chunk, capped at what the device keeps resident.
         const uint32_t grid = std::min<uint32_t>((p.nchunks + waves - 1u) / waves, (uint32_t)blocks);
         // The queue is zero here: zeroed at allocation and by every resolve pass.

@@ -65,6 +65,7 @@ struct KernelParams {
     int32_t n_pad;       // round_up(n, 4) + 4
     int32_t tiles_x;     // 8x8 pixel tiles per compact row band
     uint32_t nchunks;    // 64-item chunks of the band's work items (one item = one sample)
+    uint32_t pool_chunks;  // chunks a workgroup takes from the queue per atomic (set by launch_render)
     uint32_t items;      // band work items: passes x frame_items
     uint32_t frame_items;  // one pass's items of the band: 8x8-tile-padded pixels x spp
     uint32_t passes, pass0;  // progressive passes pass0 .. pass0 + passes - 1 in this launch
