@@ -418,3 +418,36 @@ def test_passes_argument_checks(L, O):
             dev.render_passes_async(st, L.make_params(16, 8, 5, 1 << 30, 0.5, 1, pass_=3), 2, out.data_ptr())
     finally:
         dev.release()
+
+
+@pytest.mark.parametrize("spp,radius", [(100, 0.5), (128, 0.0), (65, 2.0)])
+def test_hollow_glass_and_chunk_straddling_pixels(L, O, spp, radius):
+    """RTIOW's hollow glass sphere (a negative-radius inner sphere flips the
+    normal, ray/objects.go:100), fuzzed metal, and sample counts whose pixels
+    span or straddle 64-sample work chunks; AA disc radius 0 and 2. Linear scan
+    and BVH both against the oracle."""
+    from oracle.oracle import SPHERE_DTYPE
+
+    s = np.zeros(30, dtype=SPHERE_DTYPE)  # > kBvhMinSpheres: the BVH is built
+    rows = [((0, -100.5, -1), 100.0, 1, (0.8, 0.8, 0.0), 0.0),
+            ((0, 0, -1.2), 0.5, 1, (0.1, 0.2, 0.5), 0.0),
+            ((-1, 0, -1), 0.5, 3, (0, 0, 0), 1.5),
+            ((-1, 0, -1), -0.4, 3, (0, 0, 0), 1.5),   # hollow: inner surface, normals inward
+            ((1, 0, -1), 0.5, 2, (0.8, 0.6, 0.2), 0.3),
+            ((0.3, -0.3, -0.6), 0.15, 2, (0.9, 0.9, 0.9), 0.0)]
+    for i, (c, r, m, a, prm) in enumerate(rows):
+        s[i]["center"], s[i]["radius"], s[i]["material"], s[i]["albedo"], s[i]["param"] = c, r, m, a, prm
+    rng = np.random.default_rng(3)
+    s[6:]["center"] = np.c_[rng.uniform(-2, 2, 24), rng.uniform(-0.45, -0.35, 24), rng.uniform(-3, 0, 24)]
+    s[6:]["radius"] = rng.uniform(0.03, 0.1, 24)
+    s[6:]["material"] = rng.integers(1, 4, 24)
+    s[6:]["albedo"] = rng.uniform(0.2, 0.9, (24, 3))
+    s[6:]["param"] = np.where(s[6:]["material"] == 3, 1.5, rng.uniform(0, 0.5, 24))
+    setup = np.array([-2, 2, 1, 0, 0, -1, 0, 1, 0, 20.0, 0, 3.4, 0.1])
+    w, h = 24, 14
+    st = camera(L, setup, w, h)
+    got, seg = gpu_render(L, s, DEFAULT_BG, st, w, h, spp, 20, radius, 5)
+    ref, rseg = O.render(s, DEFAULT_BG, st.as_array(), w, h, spp, 20, radius, 5, workers=WORKERS)
+    check(got, seg, ref, rseg)
+    lin, sl = gpu_render(L, s, DEFAULT_BG, st, w, h, spp, 20, radius, 5, flags=L.FLAG_LINEAR_SCAN)
+    assert np.array_equal(sl, seg) and np.array_equal(lin, got)
