@@ -207,7 +207,8 @@ typedef struct tray_scene_info {
     int32_t n_nodes;      /* 4-wide BVH nodes */
     int32_t n_leaves;
     int32_t stack_depth;  /* traversal stack bound (entries) */
-    int32_t lds_resident; /* 1: nodes + geometry are staged in LDS; 0: read from global memory */
+    int32_t lds_resident; /* 1: nodes + geometry are staged in LDS; 2: nodes only (geometry read from
+                             global memory); 0: all read from global memory */
     int32_t n_global;     /* spheres kept out of the tree and tested first by every traversal */
     double bound;         /* M: the BVH needs every ray origin in [-M, M]^3 */
 } tray_scene_info;

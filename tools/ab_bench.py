@@ -3,15 +3,33 @@
 same data): per round every variant renders the frame once; reports the median
 and min kernel time per variant (HIP events on the launch stream).
 
-    python tools/ab_bench.py [--config c2] [--rounds 5] NAME=path/libtray_amd.so ...
+    python tools/ab_bench.py [--config c2] [--rounds 5] NAME=path/libtray_amd.so[@KEY=VAL,...] ...
+
+`@KEY=VAL,...` sets environment variables for that variant's scene upload and launches
+(e.g. TRAY_BVH_LEAF_MAX, TRAY_BVH_LDS_MODE, which the library reads at those points).
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+@contextlib.contextmanager
+def _env(env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def main():
@@ -38,16 +56,21 @@ def main():
     runs = {}
     for v in args.variants:
         name, path = v.split("=", 1)
+        path, _, envs = path.partition("@")
+        env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
         path = os.path.abspath(path)
-        runs[name] = dict(scene=_lib.DeviceScene(spheres, bg, 0, path),
-                          out=torch.empty((H, W, 3), dtype=torch.float32, device="cuda"), ms=[])
+        with _env(env):
+            scene = _lib.DeviceScene(spheres, bg, 0, path)
+        runs[name] = dict(scene=scene, env=env, out=torch.empty((H, W, 3), dtype=torch.float32, device="cuda"),
+                          ms=[])
     ref = None
     for r in range(args.rounds + 1):
         for name, st in runs.items():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            st["scene"].render_async(cam._state, params, st["out"].data_ptr(), None, stream.cuda_stream)
-            b.record(stream)
+            with _env(st["env"]):
+                a.record(stream)
+                st["scene"].render_async(cam._state, params, st["out"].data_ptr(), None, stream.cuda_stream)
+                b.record(stream)
             torch.cuda.synchronize()
             if r > 0:
                 st["ms"].append(a.elapsed_time(b))

@@ -226,23 +226,27 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         m.type = s.material;
         m.pad = 0;
     }
-    // One sphere per leaf unless the scene then no longer fits the CU's LDS,
-    // where a few spheres per leaf (fewer nodes) may still fit it.
+    // The leaf size whose LDS plan ranks best (tray_kernel.hip bvh_lds_plan),
+    // the smallest on ties: one sphere per leaf while the scene and its stack
+    // fit the CU's LDS, else a few spheres per leaf (fewer nodes).
     Bvh bvh;
     bool has_bvh = false;
     if (n >= kBvhMinSpheres) {
-        for (int leaf_max = 1; leaf_max <= kBvhLeafMax; leaf_max *= 2) {
+        int rank = -1, leaf_lo = 1, leaf_hi = kBvhLeafMax;
+        if (const char* e = getenv("TRAY_BVH_LEAF"))  // A/B: one leaf size only
+            leaf_lo = leaf_hi = std::max(1, std::min(kBvhLeafMax, atoi(e)));
+        for (int leaf_max = leaf_lo; leaf_max <= leaf_hi; leaf_max *= 2) {
             Bvh b;
             if (!build_bvh(spheres, n, &b, leaf_max)) continue;
             const int32_t cap = b.stack_max + 1;  // + the scratch slot (tray_kernel.hip Stack)
             if (bvh_scene_lds_bytes(0, 0, 0, cap) > kMaxLDSBytes) continue;  // stack alone too deep
-            const bool fits = bvh_scene_lds_bytes((int32_t)b.nodes.size(), (int32_t)b.geo.size(),
-                                                  (int32_t)b.leaves.size(), cap) <= kMaxLDSBytes;
-            if (!has_bvh || fits) {
+            const int r = bvh_lds_plan((int32_t)b.nodes.size(), (int32_t)b.geo.size(), (int32_t)b.leaves.size(), cap).rank;
+            if (r > rank) {
                 bvh = std::move(b);
                 has_bvh = true;
+                rank = r;
             }
-            if (fits) break;
+            if (rank == 4) break;
         }
     }
     tray_scene_s* sc = new tray_scene_s();
@@ -327,10 +331,7 @@ int tray_scene_get_info(tray_scene_t sc, tray_scene_info* out) {
     out->n_nodes = sc->n_nodes;
     out->n_leaves = sc->n_leaves;
     out->stack_depth = sc->has_bvh ? sc->stack_cap - 1 : 0;
-    out->lds_resident = sc->has_bvh && bvh_scene_lds_bytes(sc->n_nodes, sc->n_slots, sc->n_leaves, sc->stack_cap) <=
-                                           kMaxLDSBytes
-                            ? 1
-                            : 0;
+    out->lds_resident = sc->has_bvh ? bvh_lds_plan(sc->n_nodes, sc->n_slots, sc->n_leaves, sc->stack_cap).mode : 0;
     out->n_global = sc->n_global;
     out->bound = sc->bvh_bound;
     return TRAY_OK;

@@ -820,7 +820,9 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 // LDS bytes of `slots` stack slots of a BVH workgroup (32-bit entries).
 __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (size_t)slots * kStackSlotBytes; }
 
-template <bool kLDS, bool kBVH, bool kStats, bool kSpill>
+// kLDS: 0 scene in global memory, 1 whole scene in LDS, 2 BVH nodes + leaf table in
+// LDS with sphere geometry in global memory (scenes too big for 1; BVH only).
+template <int kLDS, bool kBVH, bool kStats, bool kSpill>
 __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
     extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
     __attribute__((address_space(3))) Uniforms* uni_lds =
@@ -859,7 +861,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         S.stride = gridDim.x * blockDim.x;
         if constexpr (kSpill) S.ovf = p.stack_ovf + blockIdx.x * blockDim.x + threadIdx.x;
         double4* scene = smem + bvh_stack_bytes(p.stack_lds) / sizeof(double4);
-        if constexpr (kLDS) {
+        if constexpr (kLDS == 1) {
             double4* lds_nodes = scene;
             double4* lds_geo = scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4));
             int32_t* lds_idx = reinterpret_cast<int32_t*>(lds_geo + p.n_slots);
@@ -876,8 +878,20 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             sv.bgeo = lds_geo;
             sv.bidx = lds_idx;
             sv.leaves = lds_leaves;
+        } else if constexpr (kLDS == 2) {
+            // [nodes][leaves]: the traversal's dependent loads stay on chip; each
+            // leaf's sphere is one 32-B global load (L2-resident).
+            double4* lds_nodes = scene;
+            int32_t* lds_leaves =
+                reinterpret_cast<int32_t*>(scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4)));
+            const double4* gn = reinterpret_cast<const double4*>(p.nodes);
+            const int n4 = p.n_nodes * (int)(sizeof(Bvh4Node) / sizeof(double4));
+            for (int i = threadIdx.x; i < n4; i += blockDim.x) lds_nodes[i] = gn[i];
+            for (int i = threadIdx.x; i < p.n_leaves; i += blockDim.x) lds_leaves[i] = p.leaves[i];
+            sv.nodes = reinterpret_cast<const Bvh4Node*>(lds_nodes);
+            sv.leaves = lds_leaves;
         }
-    } else if constexpr (kLDS) {
+    } else if constexpr (kLDS == 1) {
         for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
         sv.geo = smem;
     }
@@ -1089,15 +1103,22 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
 
 using KernelFn = void (*)(KernelParams);
 
-template <bool kBVH, bool kSpill>
-static KernelFn pick_kernel2(bool use_lds, bool stats) {
-    if (stats) return use_lds ? render_kernel<true, kBVH, true, kSpill> : render_kernel<false, kBVH, true, kSpill>;
-    return use_lds ? render_kernel<true, kBVH, false, kSpill> : render_kernel<false, kBVH, false, kSpill>;
+template <bool kBVH, bool kSpill, bool kStats>
+static KernelFn pick_kernel3(int lds_mode) {
+    if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill>;
+    if constexpr (kBVH)
+        if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill>;
+    return render_kernel<0, kBVH, kStats, kSpill>;
 }
 
-static KernelFn pick_kernel(bool use_lds, bool bvh, bool stats, bool spill) {
-    if (!bvh) return pick_kernel2<false, false>(use_lds, stats);
-    return spill ? pick_kernel2<true, true>(use_lds, stats) : pick_kernel2<true, false>(use_lds, stats);
+template <bool kBVH, bool kSpill>
+static KernelFn pick_kernel2(int lds_mode, bool stats) {
+    return stats ? pick_kernel3<kBVH, kSpill, true>(lds_mode) : pick_kernel3<kBVH, kSpill, false>(lds_mode);
+}
+
+static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool spill) {
+    if (!bvh) return pick_kernel2<false, false>(lds_mode, stats);
+    return spill ? pick_kernel2<true, true>(lds_mode, stats) : pick_kernel2<true, false>(lds_mode, stats);
 }
 
 static KernelFn pick_resolve(int fmt) {
@@ -1126,9 +1147,30 @@ static size_t scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves
     return (b + 15) / 16 * 16;
 }
 
+// The nodes-only layout (kLDS 2): nodes and leaf table.
+static size_t nodes_lds_bytes(int32_t n_nodes, int32_t n_leaves) {
+    return ((size_t)n_nodes * sizeof(Bvh4Node) + (size_t)n_leaves * sizeof(int32_t) + 15) / 16 * 16;
+}
+
 size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap) {
     return kUniformsBytes + bvh_stack_bytes(std::min(stack_cap, kStackLdsMin)) +
            scene_lds_bytes(n_nodes, n_slots, n_leaves);
+}
+
+// Ranked: whole scene and whole stack on chip (4) > nodes and whole stack (3) >
+// whole scene, stack overflowing to global memory (2) > nodes, stack overflowing
+// (1) > scene in global memory (0). A stack overflow costs more than reading
+// sphere geometry from L2 (C5, 1,939 spheres: 4-sphere leaves, nodes-only with
+// the whole stack on chip 6592 Mrays/s vs whole scene with overflow 6313).
+LdsPlan bvh_lds_plan(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap) {
+    const size_t room = kMaxLDSBytes - kUniformsBytes;
+    const size_t all = scene_lds_bytes(n_nodes, n_slots, n_leaves), nodes = nodes_lds_bytes(n_nodes, n_leaves);
+    const size_t full = bvh_stack_bytes(stack_cap), least = bvh_stack_bytes(std::min(stack_cap, kStackLdsMin));
+    if (all + full <= room) return {1, 4};
+    if (nodes + full <= room) return {2, 3};
+    if (all + least <= room) return {1, 2};
+    if (nodes + least <= room) return {2, 1};
+    return {0, 0};
 }
 
 size_t bvh_stack_overflow_bytes(int32_t stack_cap, int device) {
@@ -1179,27 +1221,36 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    bool use_lds;
+    int lds_mode;
     size_t lds;
     if (use_bvh) {
-        // Scene in LDS when it fits next to kStackLdsMin stack slots; the stack
-        // then takes what LDS is left (up to its bound), the rest spills.
-        const size_t scene = scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves);
-        use_lds = bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap) <= kMaxLDSBytes;
-        const size_t room = kMaxLDSBytes - kUniformsBytes - (use_lds ? scene : 0);
+        // Whole scene in LDS when it fits next to kStackLdsMin stack slots, else
+        // the nodes and leaf table when they fit, else nothing; the stack then
+        // takes what LDS is left (up to its bound), the rest spills.
+        lds_mode = bvh_lds_plan(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap).mode;
+        if (const char* m = getenv("TRAY_BVH_LDS_MODE")) {  // tests / A-B: force a layout that fits
+            const int want = atoi(m);
+            if (want == 0 || (want == 2 && lds_mode != 0) ||
+                (want == 1 && bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap) <= kMaxLDSBytes))
+                lds_mode = want;
+        }
+        const size_t scene = lds_mode == 1   ? scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves)
+                             : lds_mode == 2 ? nodes_lds_bytes(p.n_nodes, p.n_leaves)
+                                             : 0;
+        const size_t room = kMaxLDSBytes - kUniformsBytes - scene;
         p.stack_lds = std::min<int32_t>(p.stack_cap, (int32_t)(room / kStackSlotBytes));
         if (const char* cap = getenv("TRAY_STACK_LDS_SLOTS"))  // tests: force the overflow path
             p.stack_lds = std::min(p.stack_lds, std::max<int32_t>(kStackLdsMin, atoi(cap)));
         if (p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
-        lds = kUniformsBytes + bvh_stack_bytes(p.stack_lds) + (use_lds ? scene : 0);
+        lds = kUniformsBytes + bvh_stack_bytes(p.stack_lds) + scene;
     } else {
         const size_t geo = (size_t)p.n_pad * sizeof(double4);
-        use_lds = geo + kUniformsBytes <= kMaxLDSBytes;
-        lds = kUniformsBytes + (use_lds ? geo : 0);
+        lds_mode = geo + kUniformsBytes <= kMaxLDSBytes ? 1 : 0;
+        lds = kUniformsBytes + (lds_mode ? geo : 0);
     }
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
-    const KernelFn fn = pick_kernel(use_lds, use_bvh, stats, use_bvh && p.stack_cap > p.stack_lds);
+    const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, use_bvh && p.stack_cap > p.stack_lds);
     const KernelFn resolve = pick_resolve(p.out_format);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {

@@ -112,6 +112,13 @@ bool band_fits(int32_t width, uint64_t spp);
 // LDS the BVH kernel needs to hold the whole BVH scene (plus its traversal
 // stacks) on chip; above kMaxLDSBytes it reads the scene from global memory.
 size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap);
+// Where the BVH kernel keeps a scene: mode 1 nodes, geometry and leaf table in
+// LDS; 2 nodes and leaf table in LDS, geometry in global memory; 0 all in global
+// memory. `rank` orders plans by speed (higher is faster; tray_kernel.hip).
+struct LdsPlan {
+    int mode, rank;
+};
+LdsPlan bvh_lds_plan(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap);
 // Bytes of global stack-overflow area a render of a scene with this stack bound
 // needs on `device` (0 when the whole stack fits in LDS).
 size_t bvh_stack_overflow_bytes(int32_t stack_cap, int device);
