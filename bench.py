@@ -79,7 +79,8 @@ def main() -> int:
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--tile-rows", type=int, default=1, help="rows per interleaved tile (N > 1): 1 balances best")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-row-step", type=int, default=1, help="oracle renders every k-th row of the frame")
+    ap.add_argument("--cpu-row-step", type=int, default=0,
+                    help="oracle renders every k-th row of the frame (0: about a C2 frame's work, ~13 s)")
     ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")
     ap.add_argument("--frames-in-flight", type=int, default=None,
                     help="launches overlap this deep (own scene copy, output and stream each): a launch's "
@@ -269,7 +270,7 @@ def main() -> int:
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed,
-                                               args.cpu_row_step)
+                                               args.cpu_row_step or auto_row_step(len(spheres), W, H, spp))
     if rank == 0:
         print(json.dumps(rec), flush=True)
     for sc in scenes:
@@ -277,6 +278,12 @@ def main() -> int:
     if dist:
         dist.destroy_process_group()
     return 0
+
+
+def auto_row_step(n_spheres, W, H, spp):
+    """Row stride that keeps the CPU sample near the whole C2 frame's linear-scan
+    work (1280x720 px x r=64 x 486 spheres): C1, C2 every row; C3, C5 every 36th."""
+    return max(1, round(W * H * spp * max(n_spheres, 1) / (1280 * 720 * 64 * 486)))
 
 
 def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step):
