@@ -3,6 +3,7 @@ reference's benchmark binary (benchmark/benchmark.go:37-47; -w and -profile-cpu
 have no meaning here).
 
     python -m tray_amd [-width 1280] [-height 720] [-r 64] [-d 50] [-seed 2] [-save out.png]
+    python -m tray_amd -ansi [-s 4] ...   # main.go's terminal view, non-interactive (-exit)
 """
 from __future__ import annotations
 
@@ -10,7 +11,7 @@ import argparse
 import sys
 import time
 
-from . import png, ray
+from . import png, ray, terminal
 
 
 def main(argv=None) -> int:
@@ -21,7 +22,12 @@ def main(argv=None) -> int:
     ap.add_argument("-d", type=int, default=50, help="max depth")
     ap.add_argument("-seed", type=int, default=2)
     ap.add_argument("-save", default="out.png", help="output PNG ('' to skip)")
+    ap.add_argument("-ansi", action="store_true",
+                    help="render at -s x the terminal size and draw it in the terminal (main.go:86-131)")
+    ap.add_argument("-s", type=float, default=4, help="supersampling factor of -ansi")
     a = ap.parse_args(argv)
+    if a.ansi:
+        a.width, a.height = terminal.image_size(*terminal.terminal_size(), a.s)
     t = ray.New(a.width, a.height)
     t.Camera = ray.RichSceneCamera()
     t.NumRaysPerPixel, t.MaxDepth, t.Seed = a.r, a.d, a.seed
@@ -33,6 +39,9 @@ def main(argv=None) -> int:
           f"{a.width * a.height * a.r / dt / 1e6:.1f} Mrays/s end to end", file=sys.stderr)
     if a.save:
         png.save_png(a.save, img)
+    if a.ansi:
+        cols, rows = terminal.terminal_size()
+        print(terminal.ansi_halfblocks(terminal.scale_image(img, cols, rows * 2)))
     return 0
 
 
