@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Instruction-mix summary of tools/profile_counters*.sh passes: per counter, the
+median over the timed (non-instrumented) render_kernel launches.
+
+    python tools/pmc_mix.py gpurun_out/ev8/all --label "C2, v8" > profiles/r1_pmc_mix_v8.json
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root", help="gpu_profile_all.sh output dir (holds pmc1/, pmc2/)")
+    ap.add_argument("--label", default="")
+    a = ap.parse_args()
+    vals, kernel = {}, None
+    for f in sorted(glob.glob(os.path.join(a.root, "pmc*", "p*", "*counter_collection.csv"))):
+        per = {}
+        for row in csv.DictReader(open(f)):
+            name = row["Kernel_Name"]
+            # the timed kernel: render_kernel<mode, true, false (no stats), spill>
+            if "render_kernel" not in name or ", true, false," not in name:
+                continue
+            kernel = name
+            key = (row["Counter_Name"], row["Dispatch_Id"])
+            per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+        for (c, _), v in per.items():
+            vals.setdefault(c, []).append(v)
+    counters = {c: statistics.median(v) for c, v in sorted(vals.items())}
+    busy = counters.get("SQ_ACTIVE_INST_VALU")
+    out = {"kernel": kernel, "label": a.label,
+           "method": "tools/profile_counters.sh + profile_counters2.sh, --frames-in-flight 1, median over launches",
+           "counters": counters}
+    if busy and counters.get("SQ_THREAD_CYCLES_VALU"):
+        out["valu_lane_utilisation"] = round(counters["SQ_THREAD_CYCLES_VALU"] / (64 * busy), 3)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

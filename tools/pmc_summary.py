@@ -17,7 +17,7 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "tray::render_kernel<true, true, false, false>"
+KERNEL = "tray::render_kernel<1, true, false, false>"
 
 
 def values(path):
@@ -47,7 +47,7 @@ def main():
         shutil.copy(src, os.path.join(ROOT, "profiles", dst))
     rec = {
         "config": args.config,
-        "kernel": "tray::render_kernel<true, true, false, false> (BVH, LDS scene, no stack spill)",
+        "kernel": "tray::render_kernel<1, true, false, false> (BVH, whole scene in LDS, no stack spill)",
         "FETCH_SIZE_KB_raw": fetch_kb,
         "WRITE_SIZE_KB": write_kb,
         "fetch_bytes_corrected": fetch,
