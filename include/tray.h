@@ -203,7 +203,7 @@ int tray_scene_release(tray_scene_t scene);
 typedef struct tray_scene_info {
     int32_t n_spheres;
     int32_t has_bvh;      /* 0: every render uses the reference-order linear scan */
-    int32_t leaf_max;     /* spheres per BVH leaf (1 unless the scene must shrink to fit LDS) */
+    int32_t leaf_max;     /* spheres per BVH leaf (1, 2 or 4: the size whose LDS layout ranks best) */
     int32_t n_nodes;      /* 4-wide BVH nodes */
     int32_t n_leaves;
     int32_t stack_depth;  /* traversal stack bound (entries) */
