@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                                            [&] { return sv.bmat[T.slot]; }, st)) {
                         ++L.segments;
                         trav_begin(T, sv, L.org, L.dir);
-                    if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
+                        if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
                         state = sv.n_nodes > 0 ? kTravState : kShadeState;
                     } else {
                         state = kIdleState;
