@@ -82,26 +82,23 @@ __device__ __forceinline__ D3 sdiv_rcp(D3 v, double t, double y) {
 }
 __device__ __forceinline__ double dot(D3 u, D3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
 __device__ __forceinline__ double length_sq(D3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
-// Unit (ray/vec3.go:116-119): each component divided by the length.
-__device__ __forceinline__ D3 unit(D3 v) {
-    const double l = __builtin_sqrt(length_sq(v));
+// Unit (ray/vec3.go:116-119): each component divided by the length. `lsq` is
+// length_sq(v) when the caller already has it (same bits).
+__device__ __forceinline__ D3 unit_lsq(D3 v, double lsq) {
+    const double l = __builtin_sqrt(lsq);
     return sdiv_rcp(v, l, 1.0 / l);
 }
+__device__ __forceinline__ D3 unit(D3 v) { return unit_lsq(v, length_sq(v)); }
 __device__ __forceinline__ bool near_zero(D3 v) {
     const double s = 1e-8;
     return (__builtin_fabs(v.x) < s) && (__builtin_fabs(v.y) < s) && (__builtin_fabs(v.z) < s);
 }
-// Go math.Min special cases (-Inf first, then NaN, then signed zeros).
-__device__ __forceinline__ double go_min(double x, double y) {
-    if (__builtin_isinf(x) && x < 0) return x;
-    if (__builtin_isinf(y) && y < 0) return y;
-    if (__builtin_isnan(x) || __builtin_isnan(y)) return __builtin_nan("");
-    if (x == 0 && x == y) return __builtin_signbit(x) ? x : y;
-    return x < y ? x : y;
-}
+// math.Min(x, 1): NaN propagates, everything else compares (no signed-zero or
+// -Inf special case can change the result against the constant 1).
+__device__ __forceinline__ double go_min1(double x) { return !(x >= 1.0) ? x : 1.0; }
 __device__ __forceinline__ D3 reflect(D3 v, D3 n) { return sub(v, smul(n, 2 * dot(v, n))); }
 __device__ __forceinline__ D3 refract(D3 uv, D3 n, double eta) {
-    const double cos_theta = go_min(dot(neg(uv), n), 1.0);
+    const double cos_theta = go_min1(dot(neg(uv), n));
     const D3 perp = smul(add(uv, smul(n, cos_theta)), eta);
     const D3 par = smul(n, -__builtin_sqrt(__builtin_fabs(1.0 - length_sq(perp))));
     return add(perp, par);
@@ -626,7 +623,8 @@ __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni
 // n / d for n < 2^32 through the FP64 reciprocal (rinv = RN(1/d)): the product
 // is within 2^-20 of n/d, so its floor is off by at most one; one correction step.
 __device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t d, double rinv, uint32_t& rem) {
-    int64_t q = (int64_t)((double)n * rinv);
+    // 0 <= n * rinv < 2^32: a single v_cvt_u32_f64 (an int64 conversion is ~10 instructions)
+    int64_t q = (int64_t)(uint32_t)((double)n * rinv);
     int64_t r = (int64_t)n - q * (int64_t)d;
     if (r < 0) {
         --q;
@@ -701,14 +699,14 @@ __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D
 // direction (sky, Metal, Dielectric).
 template <bool kStats, typename GeoAt, typename MatAt>
 __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
-                                           GeoAt geo_at, MatAt mat_at, Stats& st) {
+                                           double dir_lsq, GeoAt geo_at, MatAt mat_at, Stats& st) {
     const bool hit = best >= 0;
     // A hit at the last level ends the path black whatever its material does
     // (RayColor(depth 0) is black), so no scatter is computed for it.
     const bool last = L.bounce + 1u >= (uint32_t)p.max_depth;
     bool ends = !hit || last;
     const U4 u = philox_u4(uni_seed(uni), L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
-    const D3 ud = unit(L.dir);
+    const D3 ud = unit_lsq(L.dir, dir_lsq);  // dir_lsq = length_sq(L.dir), the segment's `a`
     D3 color = d3(0, 0, 0);
     if (!hit) {  // AmbientLight.Hit (ray/objects.go:68-73)
         const double t = 0.5 * (ud.y + 1.0);
@@ -726,7 +724,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         D3 att = d3(m.albedo[0], m.albedo[1], m.albedo[2]);
         const bool lambertian = m.type == kLambertian, dielectric = m.type == kDielectric;
         // One sqrt serves RandomUnitVector's sqrt(1 - z^2) and Dielectric's sin_theta.
-        const double cos_theta = go_min(dot(neg(ud), normal), 1.0);
+        const double cos_theta = go_min1(dot(neg(ud), normal));
         const double z = 1.0 - 2.0 * u.u0;
         const double sq = __builtin_sqrt(dielectric ? 1.0 - cos_theta * cos_theta : 1.0 - z * z);
         D3 uv = d3(0, 0, 0);
@@ -972,7 +970,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 ++L.segments;
                 double closest;
                 const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
-                shade_step<kStats>(p, uni, L, best, closest, [&] { return p.geo[best]; },
+                shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[best]; },
                                    [&] { return p.mat[best]; }, st);
             }
         } else {
@@ -1017,7 +1015,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 PROF_CNT(8, 1);
                 PROF_CNT(9, __popcll(m_shade));
                 if (state == kShadeState) {
-                    if (shade_step<kStats>(p, uni, L, T.best, T.closest, [&] { return sv.bgeo[T.slot]; },
+                    if (shade_step<kStats>(p, uni, L, T.best, T.closest, T.a, [&] { return sv.bgeo[T.slot]; },
                                            [&] { return sv.bmat[T.slot]; }, st)) {
                         ++L.segments;
                         trav_begin(T, sv, L.org, L.dir);
