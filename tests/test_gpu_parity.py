@@ -304,20 +304,24 @@ def test_scene_info_and_traversal_paths(L, O):
     assert np.array_equal(sb, sl) and np.array_equal(bvh, lin)
 
 
-@pytest.mark.parametrize("seed,half,leaf,mode,resident", [(2, 11, "4", "2", 1), (2, 11, "1", "0", 1),
-                                                          (7, 22, "1", None, 0), (7, 22, "4", None, 2),
-                                                          (7, 22, "4", "1", 2), (7, 22, None, None, 2)])
-def test_bvh_lds_layouts(L, O, monkeypatch, seed, half, leaf, mode, resident):
+@pytest.mark.parametrize("seed,half,leaf,mode,resident,slots", [(2, 11, "4", "2", 1, None), (2, 11, "1", "0", 1, None),
+                                                                (7, 22, "1", None, 0, None), (7, 22, "4", None, 2, None),
+                                                                (7, 22, "4", "1", 2, None), (7, 22, None, None, 2, None),
+                                                                (7, 22, None, None, 2, "8"), (2, 11, "1", "2", 1, "8")])
+def test_bvh_lds_layouts(L, O, monkeypatch, seed, half, leaf, mode, resident, slots):
     """Every LDS layout of the BVH kernel (1: nodes + geometry; 2: nodes + leaf
     table, geometry from global memory; 0: all global), as chosen per leaf size
-    (TRAY_BVH_LEAF) or forced (TRAY_BVH_LDS_MODE), renders the linear scan's
-    bits. The dense scene (1,939 spheres) picks 2-sphere leaves, nodes-only."""
+    (TRAY_BVH_LEAF) or forced (TRAY_BVH_LDS_MODE), with the whole stack in LDS
+    or most of it in the overflow area, renders the linear scan's bits. The
+    dense scene (1,939 spheres) picks 2-sphere leaves, nodes-only."""
     sc = O.rich_scene(seed, half)
     st = camera(L, RICH_SETUP, 48, 27)
     if leaf:
         monkeypatch.setenv("TRAY_BVH_LEAF", leaf)
     if mode:
         monkeypatch.setenv("TRAY_BVH_LDS_MODE", mode)
+    if slots:  # stack partly in the global overflow area (the spill kernels)
+        monkeypatch.setenv("TRAY_STACK_LDS_SLOTS", slots)
     info = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0).info()
     assert info.has_bvh == 1 and info.lds_resident == resident
     if leaf is None:
