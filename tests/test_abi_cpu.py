@@ -193,3 +193,17 @@ def test_png_sink_round_trip():
     data = png.encode_png(img)
     assert data[:8] == b"\x89PNG\r\n\x1a\n" and data[12:16] == b"IHDR"
     assert np.array_equal(png.decode_png(data), img)
+
+
+def test_bench_cpu_sample_size():
+    """bench.py's cpu_baseline sample: every row for C1/C2 (the whole C2 frame is
+    ~13 s on 16 threads), a row stride for the larger configs that keeps the
+    oracle's linear-scan work near one C2 frame."""
+    import bench
+
+    label, seed, half, W, H, spp, depth = bench.CONFIGS["c2"]
+    assert bench.auto_row_step(486, W, H, spp) == 1
+    assert bench.auto_row_step(486, 400, 225, 16) == 1
+    assert bench.auto_row_step(1939, 1920, 1080, 256) == 36
+    assert bench.auto_row_step(486, 3840, 2160, 256) == 36
+    assert bench.auto_row_step(0, 64, 64, 1) == 1
