@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--linear", action="store_true", help="force the linear-scan kernel")
+    ap.add_argument("--half", type=int, default=None, help="override the scene's grid half-extent (density)")
+    ap.add_argument("--spp", type=int, default=None, help="override rays per pixel")
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
     import numpy as np
@@ -46,6 +48,8 @@ def main():
     from tray_amd import _lib, ray
 
     label, seed, half, W, H, spp, depth = CONFIGS[args.config]
+    half = args.half or half
+    spp = args.spp or spp
     spheres = ray.rich_scene_array(seed, half)
     cam = ray.RichSceneCamera()
     cam.Initialize(W, H)
