@@ -12,20 +12,20 @@ collective inside the render) and the frames are gathered to rank 0 by RCCL
 over xGMI ("scaling": "strong": the frame is fixed as N grows).
 value = W*H*r*steps / max-over-ranks wall time.
 Frames are progressive passes (tray_params.pass = frame index: every frame
-draws fresh samples). --passes F renders F frames per launch
-(tray_render_passes_async: lanes flow from one frame's samples into the next,
-so a launch has one tail of long paths, not F; default 1 at N = 1, 8 at N > 1,
-where a shard is ~1 ms of work and a d=50 tail would cost ~10 %), with ONE
-gather per launch. Launches rotate over --frames-in-flight slots (own device
-scene - work queue, sample buffer -, output and stream; default 3), so a
-launch's workgroups start on the CUs the previous launch's last long paths
-leave idle. Every step still renders its whole frame inside the
-timed region.
+draws fresh samples). --passes F (default 8, THE SAME AT EVERY N, so the N = 1
+line and every point of a 1 -> 8 curve share one launch shape) renders F
+frames per launch (tray_render_passes_async: lanes flow from one frame's
+samples into the next, so a launch has one tail of long paths, not F); at
+N > 1 one gather per launch moves its F frames to rank 0, on a stream of its
+own. Launches rotate over --frames-in-flight slots (own device scene - work
+queue, sample buffer -, output and stream; default 2), so a launch's
+workgroups start on the CUs the previous launch's last long paths leave idle.
+Every step still renders its whole frame inside the timed region.
 
 Also reported (rank 0):
   roofline     the megakernel against the FP64 VALU roof (it is compute and
-               latency bound; HBM traffic is far below its roof and reported
-               under "hbm"): achieved = algorithmic VALU work per launch / mean
+               latency bound; HBM traffic, by PMC, is far below its roof and is
+               reported against the algorithmic W*H*12 B per frame): achieved = algorithmic VALU work per launch / mean
                launch time, in FP64-op equivalents. No FMA is allowed in the FP64
                arithmetic, so the peak is 78.6 TFLOP/s / 2 = 39.3 T ops/s (a
                wave64 FP64 op issues in 4 cycles on a SIMD-32); an FP32 op issues
@@ -35,9 +35,16 @@ Also reported (rank 0):
                FMA + 5 min/max/compare). Segments, sphere and box tests are
                counted by the kernel itself in an untimed instrumented launch
                (segments are bit-exact with the oracle). The timed launch is the
-               megakernel plus its per-pixel resolve pass (both kernels are on the
-               stream between the two HIP events); "brute_force_equiv" rates the
-               same frame at the reference's all-spheres-per-segment work.
+               megakernel plus its per-pixel resolve passes (all on the stream
+               between the two HIP events). Beside the spec peak: the measured
+               FP64 mul+add peak, and the counter-derived VALU issue and lane
+               utilisation of this build (profiles/pmc_mix_<config>.json), which a
+               worse BVH cannot inflate. "brute_force_equiv" rates the same frame
+               at the reference's all-spheres-per-segment work (not a fraction).
+  single_launch_ms  one frame, one launch, nothing overlapped.
+  e2e          the drop-in call: one synchronous tray_render of the frame into
+               host memory as RGBA8 (what benchmark.go:88 times around
+               rt.Render), cold (BVH build, upload, allocation) and warm.
   cpu_baseline the oracle (C port of the reference's CPU loop with the
                reference's chunk-queue scheduler, ray/tracer.go:86-116) timed on
                a bounded row sample of the same frame on the host cores.
@@ -71,6 +78,31 @@ FP64_PEAK_OPS = FP64_PEAK_TFLOPS / 2  # T non-FMA FP64 ops/s (parity forbids con
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+FP64_PEAK_MEASURED = 34.03    # T v_mul_f64 + v_add_f64 per s, tools/fp64_peak.hip (profiles/r1_fp64_peak.json)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _profile_json(name, config, frames):
+    """profiles/<name>_<config>.json when it was measured on this launch shape (N = 1, F frames/launch)."""
+    path = os.path.join(ROOT, "profiles", f"{name}_{config}.json")
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if rec.get("frames_per_launch", 1) != frames:
+        return None, None
+    return rec, os.path.relpath(path, ROOT)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -79,15 +111,17 @@ def main() -> int:
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--tile-rows", type=int, default=1, help="rows per interleaved tile (N > 1): 1 balances best")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the synchronous tray_render (drop-in) timings")
+    ap.add_argument("--no-single", action="store_true", help="skip the one-frame launch timing (profiling runs)")
     ap.add_argument("--cpu-row-step", type=int, default=0,
                     help="oracle renders every k-th row of the frame (0: about a C2 frame's work, ~13 s)")
     ap.add_argument("--linear", action="store_true", help="force the reference-order linear scan (no BVH)")
-    ap.add_argument("--frames-in-flight", type=int, default=None,
+    ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="launches overlap this deep (own scene copy, output and stream each): a launch's "
-                         "blocks start on CUs the previous launch's last paths leave idle (default 3)")
-    ap.add_argument("--passes", type=int, default=None,
-                    help="frames per launch (tray_render_passes_async: consecutive progressive passes, one "
-                         "persistent launch, no per-frame tail); default 1 at N = 1, 8 at N > 1")
+                         "blocks start on CUs the previous launch's last paths leave idle")
+    ap.add_argument("--passes", type=int, default=8,
+                    help="frames per launch, the same at every N (tray_render_passes_async: consecutive "
+                         "progressive passes in one persistent launch, one tail of long paths per launch)")
     args = ap.parse_args()
 
     import torch
@@ -123,18 +157,20 @@ def main() -> int:
                               flags=_lib.FLAG_LINEAR_SCAN if args.linear else 0)
     params = shard.shard_params(params, args.tile_rows, world, rank)
     rows = _lib.params_rows(params)
-    # A step is one frame. Frames are rendered F per launch (progressive passes
-    # of tray_render_passes_async: lanes flow from one frame's samples into the
-    # next, so a launch has one tail of long paths, not F), and launches
-    # rotate over frame slots (own device scene - work queue and sample
-    # buffer -, output and stream), so launch j+1 starts on the CUs launch j's
-    # last paths leave idle. A small shard (N > 1) is dominated by those tails.
-    F = args.passes if args.passes else (1 if world == 1 else 8)
-    F = max(1, min(F, args.steps))
-    nslot = max(1, args.frames_in_flight if args.frames_in_flight else 3)
+    # A step is one frame. Frames are rendered F per launch at every N (progressive
+    # passes of tray_render_passes_async: lanes flow from one frame's samples into
+    # the next, so a launch has one tail of long paths, not F), and launches
+    # rotate over frame slots (own device scene - work queue and sample buffer -,
+    # output and stream), so launch j+1 starts on the CUs launch j's last paths
+    # leave idle. At N > 1 each launch's F frames are gathered to rank 0 with ONE
+    # gather on a stream of its own; the next launch into the same slot waits for it.
+    F = max(1, min(args.passes, args.steps))
+    nslot = max(1, args.frames_in_flight)
     scenes = [_lib.DeviceScene(spheres, bg, local_rank) for _ in range(nslot)]
     outs = [torch.empty((F, rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslot - 1)]
+    comm = torch.cuda.Stream() if world > 1 else None
+    gathered = [None] * nslot
     scene, out, stream = scenes[0], outs[0], streams[0]
 
     def launch(k, first, n):
@@ -151,14 +187,20 @@ def main() -> int:
         for i in range(first, first + count, F):
             n = min(F, first + count - i)
             k = j % nslot
+            if gathered[k] is not None:  # slot k's previous frames have left for rank 0
+                streams[k].wait_event(gathered[k])
             with torch.cuda.stream(streams[k]):
                 launch(k, i, n)
-                if world > 1:
+            if world > 1:
+                comm.wait_stream(streams[k])
+                with torch.cuda.stream(comm):
                     shard.gather_frames(outs[k][:n], H, args.tile_rows, world, rank)
+                    gathered[k] = torch.cuda.Event()
+                    gathered[k].record(comm)
             j += 1
 
-    # Untimed instrumented launch: segments, ray-sphere and ray-box tests for the roofline.
-    # One per frame of the roofline's launch (passes 0 .. F-1).
+    # Untimed instrumented launches: segments, ray-sphere and ray-box tests for the
+    # roofline, one per frame of the roofline's launch (passes 0 .. F-1).
     segments_local = sphere_tests = box_tests = 0
     for k in range(F):
         stats = torch.zeros(3, dtype=torch.int64, device="cuda")
@@ -183,15 +225,19 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # Untimed: one launch at a time, HIP events on the launch stream, for the
-    # roofline's per-launch duration (a launch renders F frames).
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
-    for a, b in ev:
-        a.record(stream)
-        launch(0, 0, F)
-        b.record(stream)
-    torch.cuda.synchronize()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # Untimed: one launch at a time, HIP events on the launch stream.
+    def launch_ms(n, reps=3):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in ev:
+            a.record(stream)
+            launch(0, 0, n)
+            b.record(stream)
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    kernel_ms = launch_ms(F)  # the timed launch shape: F frames, megakernel + F resolves
+    single_ms = kernel_ms if F == 1 else None if args.no_single else launch_ms(1)  # one frame, nothing overlapped
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -222,6 +268,7 @@ def main() -> int:
             "frames_in_flight": nslot,
             "frames_per_launch": F,
         },
+        "single_launch_ms": round(single_ms, 4) if single_ms else None,
     }
     if world > 1 and backend != "nccl":
         rec["rehearsal_backend"] = backend  # code-path check only, not a measurement
@@ -232,17 +279,13 @@ def main() -> int:
         ops = ops64 + 0.5 * ops32
         brute = 17.0 * len(spheres) * segments_local + 60.0 * segments_local + 40.0 * local_samples
         achieved = ops / (kernel_ms * 1e-3) / 1e12
-        # megakernel: one 24-B colour per sample into the sample buffer + the scene
-        # (the resolve pass then reads the buffer and writes the float3 image)
-        out_bytes = local_samples * 24 + len(spheres) * (32 + 64)
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-        if os.path.exists(pmc_path) and world == 1 and F == 1:  # measured on that launch shape
-            try:
-                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
-        rec["roofline"] = {
+        alg_bytes = rows * W * 12 * F  # the float3 frames the launch writes
+        traffic = util = pmc_src = mix_src = None
+        if world == 1:
+            pmc, pmc_src = _profile_json("pmc", args.config, F)
+            traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+            util, mix_src = _profile_json("pmc_mix", args.config, F)
+        roof = {
             "bound": "valu",
             "achieved": round(achieved, 3),
             "peak": FP64_PEAK_OPS,
@@ -251,6 +294,9 @@ def main() -> int:
             "traffic": traffic,
             "kernel_ms": round(kernel_ms, 4),
             "frames_per_launch": F,
+            "peak_measured": FP64_PEAK_MEASURED,
+            "frac_of_measured_peak": round(achieved / FP64_PEAK_MEASURED, 4),
+            "peak_measured_source": "profiles/r1_fp64_peak.json (tools/fp64_peak.hip, v_mul_f64 + v_add_f64)",
             "segments_per_launch": segments_local,
             "sphere_tests_per_launch": sphere_tests,
             "box_tests_per_launch": box_tests,
@@ -259,15 +305,25 @@ def main() -> int:
             "ops_model": "FP64-op equivalents: 17/sphere test + 60/segment + 40/sample (FP64, no FMA; SURVEY.md 8d) "
                          "+ 0.5 x 11/box test (FP32 issues at 2x FP64 on SIMD-32); "
                          "peak = 78.6 TFLOP/s FP64 vector spec / 2 = 39.3 T ops/s",
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "traffic_over_algorithmic": round(traffic / alg_bytes, 2) if traffic else None,
+            "traffic_note": "megakernel HBM bytes by PMC (FETCH_SIZE x2 + WRITE_SIZE): the 24-B colour per sample "
+                            "the resolve pass sums in sample order (DESIGN.md 5)",
+            "traversal": "linear scan" if args.linear else "exact-culling 4-wide BVH",
             "brute_force_equiv": {"ops_per_launch": brute,
                                   "TFLOPs": round(brute / (kernel_ms * 1e-3) / 1e12, 3),
-                                  "note": "reference work (every sphere tested per segment) / measured time"},
-            "traversal": "linear scan" if args.linear else "exact-culling 4-wide BVH",
-            "hbm": {"achieved_GBs": round(out_bytes / (kernel_ms * 1e-3) / 1e9, 3), "peak_GBs": HBM_PEAK_GBS,
-                    "frac": round(out_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-                    "algorithmic_bytes_per_launch": out_bytes,
-                    "note": "not the bound; megakernel only (traffic: profiles/pmc_<config>.json)"},
+                                  "note": "NOT a roofline fraction: the reference's work (every sphere tested per "
+                                          "segment) over the measured time; the BVH skips ~99.7 % of it exactly"},
         }
+        if util:
+            roof["valu_issue_util"] = util.get("valu_issue_utilisation")
+            roof["lane_util"] = util.get("valu_lane_utilisation")
+            roof["util_source"] = mix_src
+        if traffic:
+            roof["traffic_source"] = pmc_src
+        rec["roofline"] = roof
+        if world == 1 and not args.no_e2e:
+            rec["e2e"] = e2e_timings(_lib, spheres, bg, cam, W, H, depth, spp, seed)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed,
                                                args.cpu_row_step or auto_row_step(len(spheres), W, H, spp))
@@ -278,6 +334,26 @@ def main() -> int:
     if dist:
         dist.destroy_process_group()
     return 0
+
+
+def e2e_timings(_lib, spheres, bg, cam, W, H, depth, spp, seed):
+    """The drop-in call a Go caller makes instead of Tracer.Render (benchmark.go:88
+    times rt.Render): one synchronous tray_render of the whole frame into host
+    memory as RGBA8 (image.RGBA.Pix). Cold = the first call (BVH build, scene
+    upload, sample-buffer allocation, render, D2H); warm = the same scene again
+    (the library keeps the last scene it uploaded), median of 3."""
+    import numpy as np
+
+    p = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGBA8)
+    ts = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        _lib.render(spheres, bg, cam._state, p)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    warm = float(np.median(ts[1:]))
+    return {"e2e_ms_cold": round(ts[0], 3), "e2e_ms": round(warm, 3),
+            "e2e_mrays": round(W * H * spp / warm / 1e3, 1),
+            "what": "tray_render, RGBA8 into host memory; cold includes BVH build + upload + allocation"}
 
 
 def auto_row_step(n_spheres, W, H, spp):
@@ -299,7 +375,7 @@ def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step):
     dt = time.perf_counter() - t0
     samples = len(rows) * W * spp
     return {"value": round(samples / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "seconds": round(dt, 3),
+            "seconds": round(dt, 3), "cpu_model": cpu_model(),
             "sample": f"every {row_step}. row of the same frame ({len(rows)} rows x {W} px x r={spp}), "
                       f"oracle/tray_oracle.c, {cores} pthreads"}
 

@@ -121,7 +121,8 @@ typedef struct tray_camera {
 typedef enum tray_output {
     TRAY_OUT_RGB_F64 = 0, /* linear mean colour, 3 x double per pixel (parity format) */
     TRAY_OUT_RGB_F32 = 1, /* linear mean colour rounded to float, 3 x float per pixel */
-    TRAY_OUT_RGBA8 = 2    /* ColorF.ToSRGBA (ray/vec3.go:173-180) fused on device, A = 255 */
+    TRAY_OUT_RGBA8 = 2    /* ColorF.ToSRGBA (ray/vec3.go:173-180) fused on device, A = 255; the same bytes
+                             as tray_to_srgba of the TRAY_OUT_RGB_F64 frame */
 } tray_output;
 
 /* Tracer fields (ray/tracer.go:25-36) after Render's defaulting (:64-79), plus
@@ -193,6 +194,23 @@ int tray_render(const tray_sphere *spheres, int32_t n_spheres, const tray_backgr
                 const tray_camera *camera, const tray_params *params, int32_t device, void *out,
                 uint32_t *segments_out);
 
+/* Live progress of a synchronous render (Tracer.ProgressFunc, called per row
+ * while rendering, ray/tracer.go:126-128): `rows` more rows of the row set have
+ * all their samples finished. Called on the thread that called
+ * tray_render_progress, before it returns; the rows sum to the row count. */
+typedef void (*tray_progress_fn)(int32_t rows, void *user);
+
+/* tray_render with live progress: the device counts finished samples per 8-row
+ * tile row and the calling thread polls the counters (every ~0.5 ms) while the
+ * launch runs, calling progress(rows, user) as tile rows complete. progress may
+ * be NULL (then this is tray_render). The synchronous entry points keep the
+ * last scene they uploaded on each device and reuse it while the caller passes
+ * identical spheres and background (compared byte for byte); tray_shutdown()
+ * releases it. */
+int tray_render_progress(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
+                         const tray_camera *camera, const tray_params *params, int32_t device, void *out,
+                         uint32_t *segments_out, tray_progress_fn progress, void *user);
+
 /* Device-resident scene for repeated renders (the scene is read-only during
  * Render, ray/tracer.go:48). */
 int tray_scene_upload(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
@@ -241,6 +259,15 @@ int32_t tray_params_rows(const tray_params *params);
 
 /* ColorF.ToSRGBA on the host (ray/vec3.go:173-180): n_pixels linear RGB doubles -> RGBA8. */
 int tray_to_srgba(const double *rgb, size_t n_pixels, uint8_t *rgba);
+
+/* The same encoder on `device`, over DEVICE buffers (n_pixels x 3 doubles ->
+ * n_pixels x 4 bytes, A = 255), enqueued on `stream` (e.g. to encode a frame
+ * accumulated from progressive passes without a host round trip). Bit-identical
+ * to tray_to_srgba: the device counts the thresholds t[k] <= c of a 255-entry
+ * table the host derives from its own encoder (t[k] = least double encoding to
+ * >= k), so no device pow is involved. TRAY_OUT_RGBA8 renders use the same table. */
+int tray_linear_to_srgba_async(const double *rgb_device, size_t n_pixels, uint8_t *rgba_device, int32_t device,
+                               void *stream);
 
 #ifdef __cplusplus
 }

@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp, _dp]
         L.oracle_linear_to_srgb.argtypes = [ctypes.c_double]
         L.oracle_linear_to_srgb.restype = ctypes.c_uint8
+        L.oracle_linear_to_srgb_n.argtypes = [_dp, ctypes.c_size_t, _vp]
         L.oracle_camera_initialize.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp]
         L.oracle_rich_scene.argtypes = [ctypes.c_uint64, ctypes.c_int, _vp, ctypes.c_int]
         L.oracle_default_scene.argtypes = [_vp, ctypes.c_int]
@@ -171,17 +172,21 @@ def linear_to_srgb(c: float) -> int:
     return int(lib().oracle_linear_to_srgb(c))
 
 
+def linear_to_srgb_n(c: np.ndarray) -> np.ndarray:
+    """oracle_linear_to_srgb elementwise over any float64 array -> uint8 of the same shape."""
+    flat = np.ascontiguousarray(np.asarray(c, dtype=np.float64).reshape(-1))
+    out = np.empty(flat.shape[0], dtype=np.uint8)
+    lib().oracle_linear_to_srgb_n(_d(flat), flat.shape[0], out.ctypes.data)
+    return out.reshape(np.shape(c))
+
+
 def to_srgba(rgb: np.ndarray) -> np.ndarray:
-    """ColorF.ToSRGBA over an (..., 3) array -> (..., 4) uint8 (oracle scalar path)."""
-    flat = np.asarray(rgb, dtype=np.float64).reshape(-1, 3)
-    out = np.empty((flat.shape[0], 4), dtype=np.uint8)
-    f = lib().oracle_linear_to_srgb
-    for i in range(flat.shape[0]):
-        out[i, 0] = f(flat[i, 0])
-        out[i, 1] = f(flat[i, 1])
-        out[i, 2] = f(flat[i, 2])
-    out[:, 3] = 255
-    return out.reshape(np.asarray(rgb).shape[:-1] + (4,))
+    """ColorF.ToSRGBA over an (..., 3) array -> (..., 4) uint8."""
+    rgb = np.asarray(rgb, dtype=np.float64)
+    out = np.empty(rgb.shape[:-1] + (4,), dtype=np.uint8)
+    out[..., :3] = linear_to_srgb_n(rgb)
+    out[..., 3] = 255
+    return out
 
 
 def sphere_hit(sphere, origin, direction, t_start, t_end):

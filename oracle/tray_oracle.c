@@ -669,6 +669,11 @@ ORACLE_EXPORT uint8_t oracle_linear_to_srgb(double c) {
     return (uint8_t)floor(s * 255.0 + 0.5);
 }
 
+/* oracle_linear_to_srgb over n values (test sweeps of >= 10^6 channels). */
+ORACLE_EXPORT void oracle_linear_to_srgb_n(const double *c, size_t n, uint8_t *out) {
+    for (size_t i = 0; i < n; ++i) out[i] = oracle_linear_to_srgb(c[i]);
+}
+
 /* ------------------------------------------------------------------ */
 /* Host setup restatement: Camera.Initialize, RichScene, DefaultScene.  */
 /* ------------------------------------------------------------------ */

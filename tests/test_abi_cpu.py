@@ -207,3 +207,29 @@ def test_bench_cpu_sample_size():
     assert bench.auto_row_step(1939, 1920, 1080, 256) == 36
     assert bench.auto_row_step(486, 3840, 2160, 256) == 36
     assert bench.auto_row_step(0, 64, 64, 1) == 1
+
+
+def test_srgb_threshold_encoding_equals_encoder(L, O):
+    """The device's TRAY_OUT_RGBA8 encoder counts thresholds t[k] (least double
+    encoding to >= k); that equals the host/oracle encoder wherever the encoder
+    is monotone. Check monotonicity on sorted random values, the exact
+    threshold bracketing, and the host C-ABI encoder against the oracle there."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_parity import srgb_thresholds
+
+    t = srgb_thresholds(O)
+    k = np.arange(1, 256)
+    assert np.all(np.diff(t) > 0)
+    assert np.array_equal(O.linear_to_srgb_n(t).astype(int), k)
+    assert np.array_equal(O.linear_to_srgb_n(np.nextafter(t, 0)).astype(int), k - 1)
+    rng = np.random.default_rng(5)
+    v = np.sort(np.concatenate([rng.random(1_000_000), rng.random(200_000) * 0.004]))
+    enc = O.linear_to_srgb_n(v)
+    assert np.all(np.diff(enc.astype(int)) >= 0)
+    assert np.array_equal(np.searchsorted(t, v, side="right"), enc)  # count of t[k] <= c
+    rgb = v[: len(v) // 3 * 3].reshape(-1, 3)
+    host = np.zeros((len(rgb), 4), dtype=np.uint8)
+    L.check(L.lib().tray_to_srgba(rgb.ctypes.data, len(rgb), host.ctypes.data))
+    assert np.array_equal(host, O.to_srgba(rgb))

@@ -111,3 +111,34 @@ def test_render_to_png(ray, tmp_path):  # benchmark/benchmark.go:23-33: png.Enco
     path = str(tmp_path / "out.png")
     png.save_png(path, img)
     assert np.array_equal(png.decode_png(open(path, "rb").read()), img)
+
+
+def test_progress_is_live(ray):  # tracer.go:126-128: ProgressFunc per row WHILE rendering
+    """tray_render_progress reports rows as their samples finish, from device
+    counters polled during the launch: several callbacks, the first well before
+    the end, every row exactly once; Tracer.ProgressFunc sees width per row."""
+    import time
+
+    from tray_amd import _lib
+
+    W, H = 1280, 720
+    cam = ray.RichSceneCamera()
+    cam.Initialize(W, H)
+    spheres = ray.rich_scene_array(2)
+    bg = ray._background(ray.DefaultBackground())
+    p = _lib.make_params(W, H, 50, 256, 0.5, 2, output=_lib.OUT_RGB_F32)
+    _lib.render(spheres, bg, cam._state, p)  # warm: scene upload + sample buffer
+    calls = []
+    t0 = time.perf_counter()
+    _lib.render(spheres, bg, cam._state, p, progress=lambda rows: calls.append((time.perf_counter(), rows)))
+    t1 = time.perf_counter()
+    assert sum(r for _, r in calls) == H
+    assert len(calls) >= 3, calls
+    assert calls[0][1] < H and calls[0][0] < t0 + 0.8 * (t1 - t0)
+    t = ray.New(64, 36)
+    t.Camera = ray.RichSceneCamera()
+    t.NumRaysPerPixel, t.MaxDepth, t.Seed = 16, 20, 2
+    seen = []
+    t.ProgressFunc = seen.append
+    t.Render(ray.RichScene(2))
+    assert seen == [64] * 36

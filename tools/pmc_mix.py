@@ -16,6 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root", help="gpu_profile_all.sh output dir (holds pmc1/, pmc2/)")
     ap.add_argument("--label", default="")
+    ap.add_argument("--frames", type=int, default=8, help="frames per launch of the profiled bench command")
     a = ap.parse_args()
     vals, kernel = {}, None
     for f in sorted(glob.glob(os.path.join(a.root, "pmc*", "p*", "*counter_collection.csv"))):
@@ -32,11 +33,21 @@ def main():
             vals.setdefault(c, []).append(v)
     counters = {c: statistics.median(v) for c, v in sorted(vals.items())}
     busy = counters.get("SQ_ACTIVE_INST_VALU")
-    out = {"kernel": kernel, "label": a.label,
+    out = {"kernel": kernel, "label": a.label, "frames_per_launch": a.frames,
            "method": "tools/profile_counters.sh + profile_counters2.sh, --frames-in-flight 1, median over launches",
            "counters": counters}
     if busy and counters.get("SQ_THREAD_CYCLES_VALU"):
+        # active lanes per issued VALU instruction
         out["valu_lane_utilisation"] = round(counters["SQ_THREAD_CYCLES_VALU"] / (64 * busy), 3)
+    fp64 = sum(counters.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                               "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+    valu, gui = counters.get("SQ_INSTS_VALU"), counters.get("GRBM_GUI_ACTIVE")
+    if valu and gui and fp64:
+        # issue cycles of the VALU instructions (a wave64 FP64 op holds a SIMD-32 for 4 cycles,
+        # any other VALU op for 2: MI355X_MICROARCH.md) over the SIMD-cycles of the launch
+        # (256 CUs x 4 SIMDs; GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles)
+        out["valu_issue_utilisation"] = round((4 * fp64 + 2 * (valu - fp64)) / (1024 * gui / 8), 3)
+        out["fp64_share_of_valu"] = round(fp64 / valu, 3)
     print(json.dumps(out, indent=1))
 
 

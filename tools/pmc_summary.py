@@ -32,6 +32,7 @@ def main():
     ap.add_argument("profdir")
     ap.add_argument("--config", default="c2")
     ap.add_argument("--tag", required=True)
+    ap.add_argument("--frames", type=int, default=8, help="frames per launch of the profiled bench command")
     args = ap.parse_args()
     d = args.profdir
     fetch_kb = statistics.median(values(os.path.join(d, "FETCH_SIZE", "pmc_counter_collection.csv")))
@@ -47,14 +48,15 @@ def main():
         shutil.copy(src, os.path.join(ROOT, "profiles", dst))
     rec = {
         "config": args.config,
+        "frames_per_launch": args.frames,
         "kernel": "tray::render_kernel<1, true, false, false> (BVH, whole scene in LDS, no stack spill)",
         "FETCH_SIZE_KB_raw": fetch_kb,
         "WRITE_SIZE_KB": write_kb,
         "fetch_bytes_corrected": fetch,
         "write_bytes": write,
         "hbm_bytes_per_launch": int(fetch + write),
-        "note": "megakernel only; its HBM traffic is the per-sample colour buffer (24 B/sample). "
-                "The resolve kernel reads it back.",
+        "note": "megakernel only, per launch (frames_per_launch frames); its HBM traffic is the per-sample "
+                "colour buffer (24 B/sample). The resolve kernel reads it back.",
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md HBM "
                   "section: FETCH_SIZE x2 on gfx950, WRITE_SIZE exact); median over the warm launches",
         "source": [f"profiles/{v}" for v in list(copies.values())[1:]],

@@ -127,6 +127,7 @@ EXPORTS = (
     "tray_rich_scene",
     "tray_rich_scene_capacity",
     "tray_render",
+    "tray_render_progress",
     "tray_scene_upload",
     "tray_scene_release",
     "tray_scene_get_info",
@@ -135,7 +136,11 @@ EXPORTS = (
     "tray_render_stats_async",
     "tray_params_rows",
     "tray_to_srgba",
+    "tray_linear_to_srgba_async",
 )
+
+# tray_progress_fn: void (*)(int32_t rows, void *user)
+PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_void_p)
 
 _libs: dict = {}
 
@@ -165,6 +170,10 @@ def lib(path: str | None = None) -> ctypes.CDLL:
     L.tray_rich_scene_capacity.restype = i32
     L.tray_render.argtypes = [vp, i32, ctypes.POINTER(Background), ctypes.POINTER(CameraState),
                               ctypes.POINTER(Params), i32, vp, u32p]
+    if hasattr(L, "tray_render_progress"):  # absent from older builds (A/B tools)
+        L.tray_render_progress.argtypes = L.tray_render.argtypes + [PROGRESS_FN, vp]
+    if hasattr(L, "tray_linear_to_srgba_async"):
+        L.tray_linear_to_srgba_async.argtypes = [vp, ctypes.c_size_t, vp, i32, vp]
     L.tray_scene_upload.argtypes = [vp, i32, ctypes.POINTER(Background), i32, ctypes.POINTER(vp)]
     L.tray_scene_release.argtypes = [vp]
     if hasattr(L, "tray_scene_get_info"):  # absent from builds older than this binding (A/B tools)
@@ -210,9 +219,10 @@ def params_rows(p: Params) -> int:
 
 
 def render(spheres, background: Background, camera: CameraState, params: Params, device: int = 0,
-           segments: bool = False):
+           segments: bool = False, progress=None):
     """Synchronous tray_render into host memory. Returns (pixels, segments-or-None);
-    pixels is (rows, W, 3) f64 / (rows, W, 3) f32 / (rows, W, 4) u8 by params.output."""
+    pixels is (rows, W, 3) f64 / (rows, W, 3) f32 / (rows, W, 4) u8 by params.output.
+    progress(rows): called (tray_render_progress) as rows finish while the device renders."""
     s = spheres_array(spheres)
     rows = params_rows(params)
     shape = {OUT_RGB_F64: (rows, params.width, 3), OUT_RGB_F32: (rows, params.width, 3),
@@ -220,10 +230,20 @@ def render(spheres, background: Background, camera: CameraState, params: Params,
     dtype = {OUT_RGB_F64: np.float64, OUT_RGB_F32: np.float32, OUT_RGBA8: np.uint8}[params.output]
     out = np.zeros(shape, dtype=dtype)
     seg = np.zeros((rows, params.width), dtype=np.uint32) if segments else None
-    check(lib().tray_render(s.ctypes.data if len(s) else None, len(s), ctypes.byref(background),
-                            ctypes.byref(camera), ctypes.byref(params), device, out.ctypes.data,
-                            seg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) if seg is not None else None))
+    args = (s.ctypes.data if len(s) else None, len(s), ctypes.byref(background), ctypes.byref(camera),
+            ctypes.byref(params), device, out.ctypes.data,
+            seg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) if seg is not None else None)
+    if progress is None:
+        check(lib().tray_render(*args))
+    else:
+        cb = PROGRESS_FN(lambda rows, _user: progress(int(rows)))  # kept alive for the call
+        check(lib().tray_render_progress(*args, cb, None))
     return out, seg
+
+
+def linear_to_srgba_async(rgb_ptr: int, n_pixels: int, rgba_ptr: int, device: int = 0, stream: int | None = None):
+    """tray_linear_to_srgba_async: ColorF.ToSRGBA over device buffers (n x 3 f64 -> n x 4 u8)."""
+    check(lib().tray_linear_to_srgba_async(rgb_ptr, n_pixels, rgba_ptr, device, stream))
 
 
 class DeviceScene:

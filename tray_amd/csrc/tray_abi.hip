@@ -10,9 +10,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tray.h"
@@ -39,15 +41,27 @@ static int hip_fail(hipError_t e, const char* what) {
         if (e_ != hipSuccess) return hip_fail(e_, #call); \
     } while (0)
 
+// Per-device state of the synchronous entry points (tray_render*): their
+// stream and workspaces, the last scene they uploaded (reused while a caller
+// renders the same scene again, as main.go does on every resize), the progress
+// counters, and the sRGB encoder table of tray_linear_to_srgba_async.
 struct DeviceState {
     std::mutex mu;
     bool checked = false;
     bool usable = false;
     hipStream_t stream = nullptr;
+    hipStream_t poll_stream = nullptr;
     void* out_ws = nullptr;
     size_t out_ws_bytes = 0;
     uint32_t* seg_ws = nullptr;
     size_t seg_ws_bytes = 0;
+    uint32_t* prog_dev = nullptr;   // samples finished per 8-row tile row
+    uint32_t* prog_host = nullptr;  // pinned mirror the polling loop reads
+    size_t prog_bytes = 0;
+    double* srgb = nullptr;         // tray::srgb_thresholds on the device
+    tray_scene_s* cached = nullptr;  // the scene of the last tray_render call
+    std::vector<tray_sphere> cached_spheres;
+    tray_background cached_bg;
 };
 
 static std::mutex g_devices_mu;
@@ -113,6 +127,7 @@ struct tray_scene_s {
     // demand: renders of one scene must be ordered (one stream, or synchronised).
     double* samples;
     size_t samples_bytes;
+    double* srgb;  // the RGBA8 encoder table (tray::srgb_thresholds), 256 doubles
 };
 
 using namespace tray;
@@ -124,6 +139,8 @@ static int validate_spheres(const tray_sphere* s, int32_t n) {
         if (s[i].material < TRAY_LAMBERTIAN || s[i].material > TRAY_DIELECTRIC)
             return fail(TRAY_ERR_UNSUPPORTED, "sphere " + std::to_string(i) + ": unsupported material kind " +
                                                   std::to_string(s[i].material));
+        if (s[i].reserved != 0)
+            return fail(TRAY_ERR_INVALID_ARGUMENT, "sphere " + std::to_string(i) + ": reserved field must be 0");
     }
     return TRAY_OK;
 }
@@ -146,7 +163,7 @@ static int validate_params(const tray_params* p) {
         return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown output format");
     if (p->flags & ~TRAY_FLAG_LINEAR_SCAN) return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown flags");
     if (p->pass < 0) return fail(TRAY_ERR_INVALID_ARGUMENT, "pass must be >= 0");
-    if ((uint64_t)(p->pass + 1) * (uint64_t)p->rays_per_pixel > 0x100000000ull)
+    if (((uint64_t)p->pass + 1u) * (uint64_t)p->rays_per_pixel > 0x100000000ull)
         return fail(TRAY_ERR_TOO_LARGE, "pass x rays_per_pixel exceeds the 32-bit RNG sample word");
     return TRAY_OK;
 }
@@ -267,6 +284,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->bmat = nullptr;
     sc->samples = nullptr;
     sc->samples_bytes = 0;
+    sc->srgb = nullptr;
     std::vector<MatRec> bmat(bvh.idx.size());
     for (size_t i = 0; i < bvh.idx.size(); ++i) {
         const int32_t k = bvh.idx[i];
@@ -284,6 +302,8 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     if (e == hipSuccess) e = hipMalloc(&sc->queue, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(sc->queue, 0, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemcpy(sc->geo, geo.data(), sizeof(double4) * (size_t)n_pad, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&sc->srgb, 256 * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(sc->srgb, srgb_thresholds(), 256 * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess && n > 0) e = hipMalloc(&sc->mat, sizeof(MatRec) * (size_t)n);
     if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess && has_bvh) {
@@ -315,6 +335,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         (void)hipFree(sc->bgeo);
         (void)hipFree(sc->bidx);
         (void)hipFree(sc->bmat);
+        (void)hipFree(sc->srgb);
         delete sc;
         return hip_fail(e, "scene upload");
     }
@@ -350,18 +371,19 @@ int tray_scene_release(tray_scene_t sc) {
     if (sc->bidx) (void)hipFree(sc->bidx);
     if (sc->bmat) (void)hipFree(sc->bmat);
     if (sc->samples) (void)hipFree(sc->samples);
+    if (sc->srgb) (void)hipFree(sc->srgb);
     delete sc;
     return TRAY_OK;
 }
 
 static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
                              uint32_t* segments_device, unsigned long long* stats_device, void* stream,
-                             int32_t n_passes = 1) {
+                             int32_t n_passes = 1, uint32_t* progress_device = nullptr) {
     if (!sc || !cam || !out_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     int rc = validate_params(p);
     if (rc) return rc;
     if (n_passes < 1) return fail(TRAY_ERR_INVALID_ARGUMENT, "n_passes must be >= 1");
-    if ((uint64_t)(p->pass + n_passes) * (uint64_t)p->rays_per_pixel > 0x100000000ull)
+    if (((uint64_t)p->pass + (uint64_t)n_passes) * (uint64_t)p->rays_per_pixel > 0x100000000ull)
         return fail(TRAY_ERR_TOO_LARGE, "(pass + n_passes) x rays_per_pixel exceeds the 32-bit RNG sample word");
     KernelParams k;
     memset(&k, 0, sizeof(k));
@@ -398,6 +420,8 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.out_frame_bytes = (size_t)k.rows * (size_t)p->width * bytes_per_pixel(p->output);
     k.segments = segments_device;
     k.stats = stats_device;
+    k.srgb = sc->srgb;
+    k.progress = progress_device;
     k.nodes = sc->nodes;
     k.bgeo = sc->bgeo;
     k.bidx = sc->bidx;
@@ -457,8 +481,49 @@ int tray_render_stats_async(tray_scene_t sc, const tray_camera* cam, const tray_
                              stream);
 }
 
+// Grows a device workspace to `bytes` (contents not kept).
+static hipError_t grow(void** buf, size_t* have, size_t bytes) {
+    if (*have >= bytes) return hipSuccess;
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    const hipError_t e = hipMalloc(buf, bytes);
+    if (e == hipSuccess) *have = bytes;
+    return e;
+}
+
+// The scene of a tray_render* call: the device's cached upload when the caller
+// passes the same spheres and background as last time (compared byte for byte;
+// the caller's arrays are copied, never retained), else a fresh upload that
+// replaces it. Called with st->mu held.
+static int cached_scene(DeviceState* st, const tray_sphere* spheres, int32_t n, const tray_background* bg,
+                        int32_t device, tray_scene_t* out) {
+    const bool same = st->cached && (int32_t)st->cached_spheres.size() == n &&
+                      (n == 0 || memcmp(st->cached_spheres.data(), spheres, sizeof(tray_sphere) * (size_t)n) == 0) &&
+                      memcmp(&st->cached_bg, bg, sizeof(*bg)) == 0;
+    if (!same) {
+        if (st->cached) tray_scene_release(st->cached);
+        st->cached = nullptr;
+        st->cached_spheres.clear();
+        tray_scene_t sc = nullptr;
+        const int rc = tray_scene_upload(spheres, n, bg, device, &sc);
+        if (rc) return rc;
+        st->cached = sc;
+        if (n > 0) st->cached_spheres.assign(spheres, spheres + n);
+        st->cached_bg = *bg;
+    }
+    *out = st->cached;
+    return TRAY_OK;
+}
+
 int tray_render(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,
                 const tray_params* p, int32_t device, void* out, uint32_t* segments_out) {
+    return tray_render_progress(spheres, n, bg, cam, p, device, out, segments_out, nullptr, nullptr);
+}
+
+int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,
+                         const tray_params* p, int32_t device, void* out, uint32_t* segments_out,
+                         tray_progress_fn progress, void* user) {
     if (!bg || !cam || !out) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     int rc = validate_params(p);
     if (rc) return rc;
@@ -470,41 +535,100 @@ int tray_render(const tray_sphere* spheres, int32_t n, const tray_background* bg
     const int32_t rows = tray_params_rows(p);
     const size_t npix = (size_t)rows * (size_t)p->width;
     if (npix == 0) return TRAY_OK;
-    tray_scene_t sc = nullptr;
-    rc = tray_scene_upload(spheres, n, bg, device, &sc);
-    if (rc) return rc;
     std::lock_guard<std::mutex> lk(st->mu);
-    auto cleanup = [&](int code) {
-        tray_scene_release(sc);
-        return code;
-    };
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess && !st->stream) e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    tray_scene_t sc = nullptr;
+    rc = cached_scene(st, spheres, n, bg, device, &sc);
+    if (rc) return rc;
+    if (!st->stream) e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
     const size_t out_bytes = npix * bytes_per_pixel(p->output);
-    if (e == hipSuccess && st->out_ws_bytes < out_bytes) {
-        if (st->out_ws) (void)hipFree(st->out_ws);
-        st->out_ws = nullptr;
-        st->out_ws_bytes = 0;
-        e = hipMalloc(&st->out_ws, out_bytes);
-        if (e == hipSuccess) st->out_ws_bytes = out_bytes;
-    }
+    if (e == hipSuccess) e = grow(&st->out_ws, &st->out_ws_bytes, out_bytes);
     const size_t seg_bytes = npix * sizeof(uint32_t);
-    if (e == hipSuccess && segments_out && st->seg_ws_bytes < seg_bytes) {
-        if (st->seg_ws) (void)hipFree(st->seg_ws);
-        st->seg_ws = nullptr;
-        st->seg_ws_bytes = 0;
-        e = hipMalloc(&st->seg_ws, seg_bytes);
-        if (e == hipSuccess) st->seg_ws_bytes = seg_bytes;
+    if (e == hipSuccess && segments_out) e = grow(reinterpret_cast<void**>(&st->seg_ws), &st->seg_ws_bytes, seg_bytes);
+    // Progress: one counter of finished samples per 8-row tile row of the compact rows.
+    const int32_t tile_rows = (rows + 7) / 8;
+    const size_t prog_bytes = (size_t)tile_rows * sizeof(uint32_t);
+    if (e == hipSuccess && progress) {
+        if (!st->poll_stream) e = hipStreamCreateWithFlags(&st->poll_stream, hipStreamNonBlocking);
+        if (e == hipSuccess && st->prog_bytes < prog_bytes) {
+            if (st->prog_dev) (void)hipFree(st->prog_dev);
+            if (st->prog_host) (void)hipHostFree(st->prog_host);
+            st->prog_dev = nullptr;
+            st->prog_host = nullptr;
+            st->prog_bytes = 0;
+            e = hipMalloc(&st->prog_dev, prog_bytes);
+            if (e == hipSuccess) e = hipHostMalloc(&st->prog_host, prog_bytes, hipHostMallocDefault);
+            if (e == hipSuccess) st->prog_bytes = prog_bytes;
+        }
+        if (e == hipSuccess) e = hipMemsetAsync(st->prog_dev, 0, prog_bytes, st->stream);
     }
-    if (e != hipSuccess) return cleanup(hip_fail(e, "workspace"));
-    rc = tray_render_async(sc, cam, p, st->out_ws, segments_out ? st->seg_ws : nullptr, st->stream);
-    if (rc) return cleanup(rc);
+    if (e != hipSuccess) return hip_fail(e, "workspace");
+    rc = render_async_impl(sc, cam, p, st->out_ws, segments_out ? st->seg_ws : nullptr, nullptr, st->stream, 1,
+                           progress ? st->prog_dev : nullptr);
+    if (rc) return rc;
     e = hipMemcpyAsync(out, st->out_ws, out_bytes, hipMemcpyDeviceToHost, st->stream);
     if (e == hipSuccess && segments_out)
         e = hipMemcpyAsync(segments_out, st->seg_ws, seg_bytes, hipMemcpyDeviceToHost, st->stream);
+    if (e != hipSuccess) return hip_fail(e, "render");
+    if (!progress) {
+        e = hipStreamSynchronize(st->stream);
+        return e == hipSuccess ? TRAY_OK : hip_fail(e, "render");
+    }
+    // Poll the counters while the launch runs; report the rows of every tile
+    // row whose samples have all finished (ProgressFunc, ray/tracer.go:126-128).
+    const uint64_t per_row = (uint64_t)p->width * (uint64_t)p->rays_per_pixel;
+    std::vector<uint8_t> done((size_t)tile_rows, 0);
+    int32_t reported = 0;
+    while (true) {
+        e = hipStreamQuery(st->stream);
+        if (e != hipErrorNotReady) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(500));
+        e = hipMemcpyAsync(st->prog_host, st->prog_dev, prog_bytes, hipMemcpyDeviceToHost, st->poll_stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(st->poll_stream);
+        if (e != hipSuccess) break;
+        int32_t fresh = 0;
+        for (int32_t t = 0; t < tile_rows; ++t) {
+            const int32_t r = std::min(8, rows - 8 * t);
+            if (!done[(size_t)t] && (uint64_t)st->prog_host[t] >= (uint64_t)r * per_row) {
+                done[(size_t)t] = 1;
+                fresh += r;
+            }
+        }
+        if (fresh) {
+            progress(fresh, user);
+            reported += fresh;
+        }
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(st->stream);
-    if (e != hipSuccess) return cleanup(hip_fail(e, "render"));
-    return cleanup(TRAY_OK);
+    if (e != hipSuccess) return hip_fail(e, "render");
+    if (reported < rows) progress(rows - reported, user);
+    return TRAY_OK;
+}
+
+int tray_linear_to_srgba_async(const double* rgb_device, size_t n_pixels, uint8_t* rgba_device, int32_t device,
+                               void* stream) {
+    if ((!rgb_device || !rgba_device) && n_pixels) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+    DeviceState* st = nullptr;
+    int rc = device_state(device, &st);
+    if (rc) return rc;
+    TRAY_HIP(hipSetDevice(device));
+    {
+        std::lock_guard<std::mutex> lk(st->mu);
+        if (!st->srgb) {
+            double* t = nullptr;
+            TRAY_HIP(hipMalloc(&t, 256 * sizeof(double)));
+            const hipError_t e = hipMemcpy(t, srgb_thresholds(), 256 * sizeof(double), hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                (void)hipFree(t);
+                return hip_fail(e, "sRGB table");
+            }
+            st->srgb = t;
+        }
+    }
+    TRAY_HIP(launch_to_srgba(rgb_device, n_pixels, reinterpret_cast<uint32_t*>(rgba_device), st->srgb,
+                             static_cast<hipStream_t>(stream)));
+    return TRAY_OK;
 }
 
 int tray_shutdown(void) {
@@ -514,13 +638,25 @@ int tray_shutdown(void) {
         if (!st) continue;
         std::lock_guard<std::mutex> lk2(st->mu);
         (void)hipSetDevice((int)d);
+        if (st->stream) (void)hipStreamSynchronize(st->stream);
+        if (st->cached) tray_scene_release(st->cached);
         if (st->out_ws) (void)hipFree(st->out_ws);
         if (st->seg_ws) (void)hipFree(st->seg_ws);
+        if (st->prog_dev) (void)hipFree(st->prog_dev);
+        if (st->prog_host) (void)hipHostFree(st->prog_host);
+        if (st->srgb) (void)hipFree(st->srgb);
         if (st->stream) (void)hipStreamDestroy(st->stream);
+        if (st->poll_stream) (void)hipStreamDestroy(st->poll_stream);
+        st->cached = nullptr;
+        st->cached_spheres.clear();
         st->out_ws = nullptr;
         st->seg_ws = nullptr;
+        st->prog_dev = nullptr;
+        st->prog_host = nullptr;
+        st->srgb = nullptr;
         st->stream = nullptr;
-        st->out_ws_bytes = st->seg_ws_bytes = 0;
+        st->poll_stream = nullptr;
+        st->out_ws_bytes = st->seg_ws_bytes = st->prog_bytes = 0;
     }
     return TRAY_OK;
 }

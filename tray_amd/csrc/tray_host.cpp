@@ -67,6 +67,13 @@ struct SceneStream {
     double range(double lo, double hi) { return lo + (hi - lo) * float64(); }
 };
 
+}  // namespace
+
+namespace tray {
+
+// tcolor.LinearToSrgb (fortio.org/terminal v0.63.4, not vendored): IEC 61966-2-1
+// transfer, clamped, x255 rounded half up; pinned by ray/vec3_test.go:264-289
+// and the sky rows of the reference's example.png.
 uint8_t srgb8(double c) {
     if (!(c > 0.0)) return 0;
     if (c >= 1.0) return 255;
@@ -74,6 +81,34 @@ uint8_t srgb8(double c) {
     return (uint8_t)floor(s * 255.0 + 0.5);
 }
 
+// Bisection over the bit patterns of the doubles in [0, 1] (ordered like their
+// values): srgb8(0) = 0 < k and srgb8(1) = 255 >= k bracket every threshold.
+static void build_srgb_thresholds(double* t) {
+    t[0] = 0.0;
+    for (int k = 1; k < 256; ++k) {
+        uint64_t lo = 0, hi = 0x3FF0000000000000ull;  // bits of 0.0 and 1.0
+        while (hi - lo > 1) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            double c;
+            memcpy(&c, &mid, sizeof(c));
+            if (srgb8(c) >= k) hi = mid;
+            else lo = mid;
+        }
+        memcpy(&t[k], &hi, sizeof(double));
+    }
+}
+
+const double* srgb_thresholds() {
+    static double table[256];
+    static const bool built = (build_srgb_thresholds(table), true);
+    (void)built;
+    return table;
+}
+
+}  // namespace tray
+
+namespace {
+using tray::srgb8;
 }  // namespace
 
 extern "C" {

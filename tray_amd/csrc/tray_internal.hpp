@@ -1,11 +1,20 @@
 // Internal helpers shared by the C-ABI translation units.
 #pragma once
 
+#include <stdint.h>
+
 #include <string>
 
 namespace tray {
 
 // Records `msg` as tray_last_error() for the calling thread and returns `code`.
 int fail(int code, const std::string& msg);
+
+// ColorF.ToSRGBA's channel encoder on the host (ray/vec3.go:173-180).
+uint8_t srgb8(double c);
+// The device encoder's table (tray_host.cpp): t[k], k = 1..255, is the smallest
+// double c with srgb8(c) >= k (t[0] is unused). srgb8(c) is the number of
+// thresholds <= c, which is how the device encodes, bit-identical by construction.
+const double* srgb_thresholds();
 
 }  // namespace tray

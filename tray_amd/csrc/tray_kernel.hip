@@ -191,12 +191,19 @@ __device__ __forceinline__ void get_ray(const KernelParams& p, UniPtr uni, const
     }
 }
 
-// ColorF.ToSRGBA channel (ray/vec3.go:173-180), IEC 61966-2-1, half-up rounding.
-__device__ __forceinline__ uint32_t linear_to_srgb(double c) {
-    if (!(c > 0.0)) return 0u;
-    if (c >= 1.0) return 255u;
-    const double s = c <= 0.0031308 ? 12.92 * c : 1.055 * pow(c, 1.0 / 2.4) - 0.055;
-    return (uint32_t)__builtin_floor(s * 255.0 + 0.5);
+// ColorF.ToSRGBA channel (ray/vec3.go:173-180) as the number of encoder
+// thresholds <= c: t[k] (k = 1..255) is the least double the host encoder maps
+// to >= k (tray::srgb_thresholds), so this returns the host encoder's byte for
+// every double, NaN and the clamps included, with no device pow. `t` is the
+// table in LDS; eight compares of a branch-free binary search.
+__device__ __forceinline__ uint32_t srgb_encode(const double* t, double c) {
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t step = 128; step >= 1; step >>= 1) n += c >= t[n + step] ? step : 0u;
+    return n;
+}
+__device__ __forceinline__ uint32_t srgba_word(const double* t, double r, double g, double b) {
+    return srgb_encode(t, r) | (srgb_encode(t, g) << 8) | (srgb_encode(t, b) << 16) | (255u << 24);
 }
 
 // Compact output row j -> image row y (see tray_params in include/tray.h).
@@ -688,6 +695,22 @@ __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D
     L.busy = false;
 }
 
+// Live progress (tray_render_progress): the lanes whose path ended in this
+// phase add their finished samples to the counter of their 8-row tile row of
+// compact rows, one no-return atomic per distinct tile row in the wave
+// (usually one: a 64-item chunk lies within one tile row). The host polls the
+// counters while the launch runs (Tracer.ProgressFunc, ray/tracer.go:126-128).
+__device__ __forceinline__ void count_progress(const KernelParams& p, bool ended, int32_t j, uint32_t lane) {
+    uint64_t m = __ballot(ended);
+    while (m != 0ull) {
+        const uint32_t first = (uint32_t)__builtin_ctzll(m);
+        const int32_t t0 = __builtin_amdgcn_readlane(j >> 3, first);
+        const uint64_t same = __ballot(ended && (j >> 3) == t0) & m;
+        if (lane == first) atomicAdd(p.progress + t0, (uint32_t)__popcll(same));
+        m &= ~same;
+    }
+}
+
 // One recursion level of RayColor (ray/objects.go:49-62) after Scene.Hit gave
 // (best, closest): the sky on a miss, else the hit record and the material's
 // scatter. `geo_at`/`mat_at` give the hit sphere's geometry and shading record.
@@ -966,13 +989,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         }
 
         if constexpr (!kBVH) {
+            bool ended = false;
             if (L.busy) {
                 ++L.segments;
                 double closest;
                 const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
-                shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[best]; },
-                                   [&] { return p.mat[best]; }, st);
+                ended = !shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[best]; },
+                                            [&] { return p.mat[best]; }, st);
             }
+            if (p.progress) count_progress(p, ended, L.j, lane);
         } else {
             // Node steps for the traversing lanes.
             {
@@ -1014,6 +1039,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 PROF_T0();
                 PROF_CNT(8, 1);
                 PROF_CNT(9, __popcll(m_shade));
+                bool ended = false;
                 if (state == kShadeState) {
                     if (shade_step<kStats>(p, uni, L, T.best, T.closest, T.a, [&] { return sv.bgeo[T.slot]; },
                                            [&] { return sv.bmat[T.slot]; }, st)) {
@@ -1023,8 +1049,10 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         state = sv.n_nodes > 0 ? kTravState : kShadeState;
                     } else {
                         state = kIdleState;
+                        ended = true;
                     }
                 }
+                if (p.progress) count_progress(p, ended, L.j, lane);
                 PROF_ADD(3);
             }
         }
@@ -1059,6 +1087,11 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 // blockIdx.y is the pass within the launch.
 template <int kFmt>
 __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
+    __shared__ double srgb[256];
+    if constexpr (kFmt == kOutRGBA8) {  // the encoder table, one entry per thread
+        srgb[threadIdx.x] = p.srgb[threadIdx.x];
+        __syncthreads();
+    }
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q == 0 && blockIdx.y == 0) *p.queue = 0u;
     if (q >= p.frame_items / (uint32_t)p.spp) return;
@@ -1093,10 +1126,26 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
         o[1] = (float)mean.y;
         o[2] = (float)mean.z;
     } else {
-        const uint32_t rgba = linear_to_srgb(mean.x) | (linear_to_srgb(mean.y) << 8) |
-                              (linear_to_srgb(mean.z) << 16) | (255u << 24);
-        static_cast<uint32_t*>(out)[off] = rgba;
+        static_cast<uint32_t*>(out)[off] = srgba_word(srgb, mean.x, mean.y, mean.z);
     }
+}
+
+// ColorF.ToSRGBA over a device buffer of linear colours (tray_linear_to_srgba_async).
+__global__ __launch_bounds__(256) void to_srgba_kernel(const double* rgb, size_t n, uint32_t* rgba,
+                                                      const double* table) {
+    __shared__ double srgb[256];
+    srgb[threadIdx.x] = table[threadIdx.x];
+    __syncthreads();
+    for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (size_t)gridDim.x * 256u)
+        rgba[i] = srgba_word(srgb, rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2]);
+}
+
+hipError_t launch_to_srgba(const double* rgb, size_t n_pixels, uint32_t* rgba, const double* srgb,
+                           hipStream_t stream) {
+    if (n_pixels == 0) return hipSuccess;
+    const size_t blocks = std::min<size_t>((n_pixels + 255) / 256, 4096);
+    hipLaunchKernelGGL(to_srgba_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, rgb, n_pixels, rgba, srgb);
+    return hipGetLastError();
 }
 
 using KernelFn = void (*)(KernelParams);

@@ -96,9 +96,17 @@ struct KernelParams {
     V3 bg_a, bg_b;
     void* out;
     uint32_t* segments;
+    const double* srgb;  // TRAY_OUT_RGBA8: the 256-entry encoder table (tray::srgb_thresholds)
+    uint32_t* progress;  // nullable: samples finished per 8-row tile row of the compact rows
 };
 
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
+
+// ColorF.ToSRGBA over n device pixels (3 doubles each) into RGBA8 words, with the
+// threshold table `srgb` (device, 256 doubles) that makes it bit-identical to the
+// host encoder.
+hipError_t launch_to_srgba(const double* rgb, size_t n_pixels, uint32_t* rgba, const double* srgb,
+                           hipStream_t stream);
 
 // Samples per launch band (the sample buffer holds one band: 24 B per sample);
 // the TRAY_BAND_SAMPLES environment variable lowers it (tests exercise bands).

@@ -256,16 +256,18 @@ class Tracer:  # ray/tracer.go:25-36
     def _render_rows(self, y0: int, y1: int, scene: Scene) -> None:
         params = _lib.make_params(self.width, self.height, self.MaxDepth, self.NumRaysPerPixel, self.RayRadius,
                                   self._seed(), y0, y1)
+        progress = None
+        if self.ProgressFunc is not None:  # per row, while the device renders (tracer.go:126-128)
+            def progress(rows):
+                for _ in range(rows):
+                    self.ProgressFunc(self.width)
         rgb, seg = _lib.render(scene.to_array(), _background(scene.Background), self.Camera._state, params,
-                               self.Device, segments=True)
+                               self.Device, segments=True, progress=progress)
         self.linear[y0:y1] = rgb
         self.segments[y0:y1] = seg
         rgba = np.zeros((y1 - y0, self.width, 4), dtype=np.uint8)
         _lib.check(_lib.lib().tray_to_srgba(rgb.ctypes.data, rgb.shape[0] * rgb.shape[1], rgba.ctypes.data))
         self.imageData[y0:y1] = rgba
-        if self.ProgressFunc is not None:
-            for _ in range(y1 - y0):
-                self.ProgressFunc(self.width)
 
     def Render(self, scene: Scene | None) -> np.ndarray:  # ray/tracer.go:48-118
         scene = self._apply_defaults(scene)

@@ -51,6 +51,11 @@ def gather_frames(local, height: int, tile_rows: int, world: int, rank: int, dst
     import torch
     import torch.distributed as dist
 
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo gathers host tensors only (RCCL, the nccl backend, gathers device
+        # memory directly over xGMI): stage through the host, hand back a device frame.
+        full = gather_frames(local.cpu(), height, tile_rows, world, rank, dst, group)
+        return None if full is None else full.to(local.device)
     counts = [len(rows_for(height, tile_rows, world, r)) for r in range(world)]
     max_rows = max(counts)
     pad = local
