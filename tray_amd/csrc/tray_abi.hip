@@ -50,13 +50,12 @@ struct DeviceState {
     bool checked = false;
     bool usable = false;
     hipStream_t stream = nullptr;
-    hipStream_t poll_stream = nullptr;
     void* out_ws = nullptr;
     size_t out_ws_bytes = 0;
     uint32_t* seg_ws = nullptr;
     size_t seg_ws_bytes = 0;
-    uint32_t* prog_dev = nullptr;   // samples finished per 8-row tile row
-    uint32_t* prog_host = nullptr;  // pinned mirror the polling loop reads
+    uint32_t* prog_host = nullptr;  // samples finished per 8-row tile row (host-mapped, coherent)
+    uint32_t* prog_dev = nullptr;   // its device address
     size_t prog_bytes = 0;
     double* srgb = nullptr;         // tray::srgb_thresholds on the device
     tray_scene_s* cached = nullptr;  // the scene of the last tray_render call
@@ -549,20 +548,18 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
     // Progress: one counter of finished samples per 8-row tile row of the compact rows.
     const int32_t tile_rows = (rows + 7) / 8;
     const size_t prog_bytes = (size_t)tile_rows * sizeof(uint32_t);
-    if (e == hipSuccess && progress) {
-        if (!st->poll_stream) e = hipStreamCreateWithFlags(&st->poll_stream, hipStreamNonBlocking);
-        if (e == hipSuccess && st->prog_bytes < prog_bytes) {
-            if (st->prog_dev) (void)hipFree(st->prog_dev);
-            if (st->prog_host) (void)hipHostFree(st->prog_host);
-            st->prog_dev = nullptr;
-            st->prog_host = nullptr;
-            st->prog_bytes = 0;
-            e = hipMalloc(&st->prog_dev, prog_bytes);
-            if (e == hipSuccess) e = hipHostMalloc(&st->prog_host, prog_bytes, hipHostMallocDefault);
-            if (e == hipSuccess) st->prog_bytes = prog_bytes;
-        }
-        if (e == hipSuccess) e = hipMemsetAsync(st->prog_dev, 0, prog_bytes, st->stream);
+    if (e == hipSuccess && progress && st->prog_bytes < prog_bytes) {
+        // counters in host memory the kernel adds to (system-scope atomics) and this
+        // thread reads: a device-to-host copy would queue behind the persistent grid
+        if (st->prog_host) (void)hipHostFree(st->prog_host);
+        st->prog_host = nullptr;
+        st->prog_dev = nullptr;
+        st->prog_bytes = 0;
+        e = hipHostMalloc(&st->prog_host, prog_bytes, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&st->prog_dev), st->prog_host, 0);
+        if (e == hipSuccess) st->prog_bytes = prog_bytes;
     }
+    if (e == hipSuccess && progress) memset(st->prog_host, 0, prog_bytes);  // the stream is idle here
     if (e != hipSuccess) return hip_fail(e, "workspace");
     rc = render_async_impl(sc, cam, p, st->out_ws, segments_out ? st->seg_ws : nullptr, nullptr, st->stream, 1,
                            progress ? st->prog_dev : nullptr);
@@ -580,17 +577,15 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
     const uint64_t per_row = (uint64_t)p->width * (uint64_t)p->rays_per_pixel;
     std::vector<uint8_t> done((size_t)tile_rows, 0);
     int32_t reported = 0;
+    const volatile uint32_t* counts = st->prog_host;
     while (true) {
         e = hipStreamQuery(st->stream);
         if (e != hipErrorNotReady) break;
         std::this_thread::sleep_for(std::chrono::microseconds(500));
-        e = hipMemcpyAsync(st->prog_host, st->prog_dev, prog_bytes, hipMemcpyDeviceToHost, st->poll_stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(st->poll_stream);
-        if (e != hipSuccess) break;
         int32_t fresh = 0;
         for (int32_t t = 0; t < tile_rows; ++t) {
             const int32_t r = std::min(8, rows - 8 * t);
-            if (!done[(size_t)t] && (uint64_t)st->prog_host[t] >= (uint64_t)r * per_row) {
+            if (!done[(size_t)t] && (uint64_t)counts[t] >= (uint64_t)r * per_row) {
                 done[(size_t)t] = 1;
                 fresh += r;
             }
@@ -642,11 +637,9 @@ int tray_shutdown(void) {
         if (st->cached) tray_scene_release(st->cached);
         if (st->out_ws) (void)hipFree(st->out_ws);
         if (st->seg_ws) (void)hipFree(st->seg_ws);
-        if (st->prog_dev) (void)hipFree(st->prog_dev);
         if (st->prog_host) (void)hipHostFree(st->prog_host);
         if (st->srgb) (void)hipFree(st->srgb);
         if (st->stream) (void)hipStreamDestroy(st->stream);
-        if (st->poll_stream) (void)hipStreamDestroy(st->poll_stream);
         st->cached = nullptr;
         st->cached_spheres.clear();
         st->out_ws = nullptr;
@@ -655,7 +648,6 @@ int tray_shutdown(void) {
         st->prog_host = nullptr;
         st->srgb = nullptr;
         st->stream = nullptr;
-        st->poll_stream = nullptr;
         st->out_ws_bytes = st->seg_ws_bytes = st->prog_bytes = 0;
     }
     return TRAY_OK;

@@ -695,18 +695,30 @@ __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D
     L.busy = false;
 }
 
-// Live progress (tray_render_progress): the lanes whose path ended in this
-// phase add their finished samples to the counter of their 8-row tile row of
-// compact rows, one no-return atomic per distinct tile row in the wave
-// (usually one: a 64-item chunk lies within one tile row). The host polls the
-// counters while the launch runs (Tracer.ProgressFunc, ray/tracer.go:126-128).
-__device__ __forceinline__ void count_progress(const KernelParams& p, bool ended, int32_t j, uint32_t lane) {
+// Live progress (tray_render_progress): finished samples per 8-row tile row of
+// compact rows, counted in HOST memory the calling thread polls while the
+// launch runs (Tracer.ProgressFunc, ray/tracer.go:126-128; no device copy can
+// run beside a persistent grid that holds every CU). A wave accumulates the
+// count of its current tile row (wave-uniform `cur`, `cnt`) and adds it to the
+// host counter with one system-scope atomic when its lanes move on to another
+// tile row (a 64-item chunk lies within one tile row) and when it exits.
+__device__ __forceinline__ void flush_progress(const KernelParams& p, int32_t t, uint32_t n, uint32_t lane) {
+    if (n != 0u && lane == 0u)
+        __hip_atomic_fetch_add(p.progress + t, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void count_progress(const KernelParams& p, bool ended, int32_t j, uint32_t lane,
+                                               int32_t& cur, uint32_t& cnt) {
     uint64_t m = __ballot(ended);
     while (m != 0ull) {
         const uint32_t first = (uint32_t)__builtin_ctzll(m);
         const int32_t t0 = __builtin_amdgcn_readlane(j >> 3, first);
         const uint64_t same = __ballot(ended && (j >> 3) == t0) & m;
-        if (lane == first) atomicAdd(p.progress + t0, (uint32_t)__popcll(same));
+        if (t0 != cur) {
+            flush_progress(p, cur, cnt, lane);
+            cur = t0;
+            cnt = 0u;
+        }
+        cnt += (uint32_t)__popcll(same);
         m &= ~same;
     }
 }
@@ -926,6 +938,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     uint32_t state = kIdleState;
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
     bool exhausted = false;
+    int32_t prog_cur = 0;  // live progress: the wave's current tile row and its unflushed count
+    uint32_t prog_cnt = 0;
 #ifdef TRAY_PROFILE
     __shared__ unsigned long long prof_lds[16 * 16];
     unsigned long long* prof = prof_lds + 16 * (threadIdx.x / 64u);
@@ -997,7 +1011,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 ended = !shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[best]; },
                                             [&] { return p.mat[best]; }, st);
             }
-            if (p.progress) count_progress(p, ended, L.j, lane);
+            if (p.progress) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
         } else {
             // Node steps for the traversing lanes.
             {
@@ -1052,11 +1066,12 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         ended = true;
                     }
                 }
-                if (p.progress) count_progress(p, ended, L.j, lane);
+                if (p.progress) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
                 PROF_ADD(3);
             }
         }
     }
+    if (p.progress) flush_progress(p, prog_cur, prog_cnt, lane);
     if constexpr (kStats) {
         atomicAdd(p.stats + 0, (unsigned long long)st.segments);
         atomicAdd(p.stats + 1, (unsigned long long)st.spheres);

@@ -97,7 +97,7 @@ struct KernelParams {
     void* out;
     uint32_t* segments;
     const double* srgb;  // TRAY_OUT_RGBA8: the 256-entry encoder table (tray::srgb_thresholds)
-    uint32_t* progress;  // nullable: samples finished per 8-row tile row of the compact rows
+    uint32_t* progress;  // nullable, HOST-mapped: samples finished per 8-row tile row of the compact rows
 };
 
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
