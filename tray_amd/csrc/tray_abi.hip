@@ -564,40 +564,37 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
     rc = render_async_impl(sc, cam, p, st->out_ws, segments_out ? st->seg_ws : nullptr, nullptr, st->stream, 1,
                            progress ? st->prog_dev : nullptr);
     if (rc) return rc;
+    // Poll the counters while the launch runs and report the rows of every tile
+    // row whose samples have all finished (ProgressFunc, ray/tracer.go:126-128).
+    // Before the copies: a copy into pageable caller memory returns only once done.
+    int32_t reported = 0;
+    if (progress) {
+        const uint64_t per_row = (uint64_t)p->width * (uint64_t)p->rays_per_pixel;
+        std::vector<uint8_t> done((size_t)tile_rows, 0);
+        const volatile uint32_t* counts = st->prog_host;
+        while ((e = hipStreamQuery(st->stream)) == hipErrorNotReady) {
+            std::this_thread::sleep_for(std::chrono::microseconds(500));
+            int32_t fresh = 0;
+            for (int32_t t = 0; t < tile_rows; ++t) {
+                const int32_t r = std::min(8, rows - 8 * t);
+                if (!done[(size_t)t] && (uint64_t)counts[t] >= (uint64_t)r * per_row) {
+                    done[(size_t)t] = 1;
+                    fresh += r;
+                }
+            }
+            if (fresh) {
+                progress(fresh, user);
+                reported += fresh;
+            }
+        }
+        if (e != hipSuccess) return hip_fail(e, "render");
+    }
     e = hipMemcpyAsync(out, st->out_ws, out_bytes, hipMemcpyDeviceToHost, st->stream);
     if (e == hipSuccess && segments_out)
         e = hipMemcpyAsync(segments_out, st->seg_ws, seg_bytes, hipMemcpyDeviceToHost, st->stream);
-    if (e != hipSuccess) return hip_fail(e, "render");
-    if (!progress) {
-        e = hipStreamSynchronize(st->stream);
-        return e == hipSuccess ? TRAY_OK : hip_fail(e, "render");
-    }
-    // Poll the counters while the launch runs; report the rows of every tile
-    // row whose samples have all finished (ProgressFunc, ray/tracer.go:126-128).
-    const uint64_t per_row = (uint64_t)p->width * (uint64_t)p->rays_per_pixel;
-    std::vector<uint8_t> done((size_t)tile_rows, 0);
-    int32_t reported = 0;
-    const volatile uint32_t* counts = st->prog_host;
-    while (true) {
-        e = hipStreamQuery(st->stream);
-        if (e != hipErrorNotReady) break;
-        std::this_thread::sleep_for(std::chrono::microseconds(500));
-        int32_t fresh = 0;
-        for (int32_t t = 0; t < tile_rows; ++t) {
-            const int32_t r = std::min(8, rows - 8 * t);
-            if (!done[(size_t)t] && (uint64_t)counts[t] >= (uint64_t)r * per_row) {
-                done[(size_t)t] = 1;
-                fresh += r;
-            }
-        }
-        if (fresh) {
-            progress(fresh, user);
-            reported += fresh;
-        }
-    }
     if (e == hipSuccess) e = hipStreamSynchronize(st->stream);
     if (e != hipSuccess) return hip_fail(e, "render");
-    if (reported < rows) progress(rows - reported, user);
+    if (progress && reported < rows) progress(rows - reported, user);
     return TRAY_OK;
 }
 
