@@ -81,6 +81,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_linear_to_srgb.argtypes = [ctypes.c_double]
         L.oracle_linear_to_srgb.restype = ctypes.c_uint8
         L.oracle_linear_to_srgb_n.argtypes = [_dp, ctypes.c_size_t, _vp]
+        L.oracle_go_tan.argtypes = [ctypes.c_double]
+        L.oracle_go_tan.restype = ctypes.c_double
         L.oracle_camera_initialize.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp]
         L.oracle_rich_scene.argtypes = [ctypes.c_uint64, ctypes.c_int, _vp, ctypes.c_int]
         L.oracle_default_scene.argtypes = [_vp, ctypes.c_int]
@@ -170,6 +172,11 @@ def unit(v) -> np.ndarray:
 
 def linear_to_srgb(c: float) -> int:
     return int(lib().oracle_linear_to_srgb(c))
+
+
+def go_tan(x: float) -> float:
+    """Go's math.Tan as restated for Camera.Initialize (ray/camera.go:93)."""
+    return float(lib().oracle_go_tan(x))
 
 
 def linear_to_srgb_n(c: np.ndarray) -> np.ndarray:

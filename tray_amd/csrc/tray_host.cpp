@@ -59,6 +59,42 @@ void set_sphere(tray_sphere* s, const Vec& c, double r, int32_t mat, const Vec& 
     s->material = mat;
 }
 
+// math.Tan of the reference's Go toolchain (Go src/math/tan.go: Cephes tan.c
+// coefficients, Pi/4 in three parts, no FMA as on GOAMD64=v1). Go's toolchain
+// is absent here, so this restates its published algorithm; each constant
+// below matches the bit pattern Go's source gives beside it (checked by
+// tests/test_abi_cpu.py). |x| >= 2^29 needs Go's Payne-Hanek reduction, which
+// is not restated: libm tan serves those (no camera reaches them).
+static double go_tan(double x) {
+    static const double P[3] = {-1.30936939181383777646e4, 1.15351664838587416140e6, -1.79565251976484877988e7};
+    static const double Q[5] = {1.0, 1.36812963470692954678e4, -1.32089234440210967447e6, 2.50083801823357915839e7,
+                                -5.38695755929454629881e7};
+    const double PI4A = 7.85398125648498535156e-1, PI4B = 3.77489470793079817668e-8,
+                 PI4C = 2.69515142907905952645e-15;
+    if (x == 0 || x != x) return x;
+    if (x - x != 0) return NAN; /* +-Inf */
+    int sign = 0;
+    if (x < 0) {
+        x = -x;
+        sign = 1;
+    }
+    if (x >= 536870912.0) return sign ? -tan(x) : tan(x);
+    uint64_t j = (uint64_t)(x * 0x1.45f306dc9c883p+0); /* x * (4/Pi), 4/Pi rounded once as Go folds it */
+    double y = (double)j;
+    if (j & 1) {
+        j++;
+        y++;
+    }
+    const double z = ((x - y * PI4A) - y * PI4B) - y * PI4C;
+    const double zz = z * z;
+    if (zz > 1e-14)
+        y = z + z * (zz * (((P[0] * zz) + P[1]) * zz + P[2]) / ((((zz + Q[1]) * zz + Q[2]) * zz + Q[3]) * zz + Q[4]));
+    else
+        y = z;
+    if (j & 2) y = -1 / y;
+    return sign ? -y : y;
+}
+
 // Sequential draws of the scene-generation stream (counter RNG purpose 4).
 struct SceneStream {
     uint64_t seed;
@@ -131,7 +167,7 @@ int tray_camera_initialize(tray_camera_setup* c, int32_t width, int32_t height, 
     const double defocus_radius = c->aperture / 2;
     // math.Pi/180 is folded by Go at arbitrary precision: the correctly rounded double.
     const double theta = c->vertical_fov * 0x1.1df46a2529d39p-6;
-    const double viewport_h = 2.0 * c->focal_length * tan(theta / 2.0);
+    const double viewport_h = 2.0 * c->focal_length * go_tan(theta / 2.0);
     const double aspect = (double)width / (double)height;
     const double viewport_w = aspect * viewport_h;
     const Vec horizontal = vscale(u, viewport_w);
