@@ -69,6 +69,36 @@ def reflect(v, n):  # Sub(v, SMul(n, 2*Dot(v, n)))
 
 
 # -------------------------------------------------------- camera.go (host) ----
+_TAN_P = (-1.30936939181383777646e4, 1.15351664838587416140e6, -1.79565251976484877988e7)
+_TAN_Q = (1.0, 1.36812963470692954678e4, -1.32089234440210967447e6, 2.50083801823357915839e7,
+          -5.38695755929454629881e7)
+
+
+def go_tan(x):
+    """Go's math.Tan (src/math/tan.go, Cephes coefficients; no FMA, as GOAMD64=v1
+    compiles it) for |x| < 2^29, in Python floats (IEEE binary64)."""
+    pi4a, pi4b, pi4c = 7.85398125648498535156e-1, 3.77489470793079817668e-8, 2.69515142907905952645e-15
+    if x == 0 or x != x:
+        return x
+    sign = x < 0
+    x = -x if sign else x
+    assert x < 2.0 ** 29
+    j = int(x * float.fromhex("0x1.45f306dc9c883p+0"))  # x * (4/Pi), the constant rounded once
+    y = float(j)
+    if j & 1:
+        j, y = j + 1, y + 1
+    z = ((x - y * pi4a) - y * pi4b) - y * pi4c
+    zz = z * z
+    if zz > 1e-14:
+        y = z + z * (zz * (((_TAN_P[0] * zz) + _TAN_P[1]) * zz + _TAN_P[2])
+                     / ((((zz + _TAN_Q[1]) * zz + _TAN_Q[2]) * zz + _TAN_Q[3]) * zz + _TAN_Q[4]))
+    else:
+        y = z
+    if j & 2:
+        y = -1 / y
+    return -y if sign else y
+
+
 def camera_initialize(position, look_at, up, vfov, focal, width, height):
     f64 = np.float64
     position = tuple(f64(c) for c in position)
@@ -76,8 +106,8 @@ def camera_initialize(position, look_at, up, vfov, focal, width, height):
     w = unit(view)
     u = unit(cross(tuple(f64(c) for c in up), w))
     v = cross(w, u)
-    theta = f64(vfov) * f64(math.pi / 180.0)
-    viewport_h = f64(2.0) * f64(focal) * f64(math.tan(theta / f64(2.0)))
+    theta = f64(vfov) * f64(float.fromhex("0x1.1df46a2529d39p-6"))  # math.Pi/180, folded exactly by Go
+    viewport_h = f64(2.0) * f64(focal) * f64(go_tan(float(theta / f64(2.0))))
     viewport_w = (f64(width) / f64(height)) * viewport_h
     horizontal = smul(u, viewport_w)
     vertical = smul(v, -viewport_h)

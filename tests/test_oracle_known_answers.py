@@ -2,6 +2,7 @@
 tests (fortio/tray ray/*_test.go) and the published Philox KAT vectors.
 CPU only; no GPU, no product code."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -235,3 +236,39 @@ def test_get_ray_pixel_center_and_offset(O):  # ray/camera_test.go:177-243
     assert O.near_zero(O.unit(target - cam[0:3]) - O.unit(d))
     _, d2 = O.get_ray(cam, 5, 5, 0.3, 0.2)
     assert tuple(d2) != tuple(d)
+
+
+def test_go_math_tan_restatement(O):
+    """Camera.Initialize's math.Tan (ray/camera.go:93) is Go's Cephes-based
+    algorithm, not libm's: the C restatement (oracle; the host copy is checked
+    against the oracle through tray_camera_initialize) equals the independent
+    Python restatement in tests/golden/make_golden.py bit for bit, stays within
+    2 ulp of the correctly rounded tangent, and reproduces Go's own
+    tan(Pi/4) = 1 where libm gives 1 - 2^-53."""
+    import math
+    import struct
+    import sys
+
+    from conftest import ROOT
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden
+
+    def bits(v):
+        return struct.unpack("<q", struct.pack("<d", v))[0]
+
+    # Go's tan.go prints each coefficient's bit pattern beside its decimal value
+    for v, h in zip(make_golden._TAN_P + make_golden._TAN_Q[1:],
+                    (0xc0c992d8d24f3f38, 0x413199eca5fc9ddd, 0xc1711fead3299176, 0x40cab8a5eeb36572,
+                     0xc13427bc582abc96, 0x4177d98fc2ead8ef, 0xc189afe03cbe5a31)):
+        assert bits(v) & (2**64 - 1) == h
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.uniform(-1.6, 1.6, 20000), rng.uniform(-50, 50, 5000),
+                         np.arange(1, 180) * float.fromhex("0x1.1df46a2529d39p-6") / 2])
+    for x in xs:
+        a, b = O.go_tan(float(x)), make_golden.go_tan(float(x))
+        assert a == b
+        assert abs(bits(a) - bits(math.tan(float(x)))) <= 2
+    quarter = 45 * float.fromhex("0x1.1df46a2529d39p-6")  # vertical_fov 90 (the default) / 2
+    assert O.go_tan(quarter) == 1.0 and math.tan(quarter) == 1.0 - 2.0 ** -53
+    assert O.go_tan(0.0) == 0.0 and math.isnan(O.go_tan(float("nan"))) and math.isnan(O.go_tan(float("inf")))
