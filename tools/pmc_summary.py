@@ -17,7 +17,7 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "tray::render_kernel<1, true, false, false>"
+KERNEL = "tray::render_kernel<1, true, false, false, false>"
 
 
 def values(path):
@@ -49,7 +49,7 @@ def main():
     rec = {
         "config": args.config,
         "frames_per_launch": args.frames,
-        "kernel": "tray::render_kernel<1, true, false, false> (BVH, whole scene in LDS, no stack spill)",
+        "kernel": "tray::render_kernel<1, true, false, false, false> (BVH, whole scene in LDS, no stack spill)",
         "FETCH_SIZE_KB_raw": fetch_kb,
         "WRITE_SIZE_KB": write_kb,
         "fetch_bytes_corrected": fetch,

@@ -855,7 +855,9 @@ __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (si
 
 // kLDS: 0 scene in global memory, 1 whole scene in LDS, 2 BVH nodes + leaf table in
 // LDS with sphere geometry in global memory (scenes too big for 1; BVH only).
-template <int kLDS, bool kBVH, bool kStats, bool kSpill>
+// kProg: the live-progress instance (tray_render_progress only), so the other
+// instances carry no progress code or registers.
+template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg>
 __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
     extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
     __attribute__((address_space(3))) Uniforms* uni_lds =
@@ -1011,7 +1013,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 ended = !shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[best]; },
                                             [&] { return p.mat[best]; }, st);
             }
-            if (p.progress) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
+            if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
         } else {
             // Node steps for the traversing lanes.
             {
@@ -1066,12 +1068,12 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         ended = true;
                     }
                 }
-                if (p.progress) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
+                if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
                 PROF_ADD(3);
             }
         }
     }
-    if (p.progress) flush_progress(p, prog_cur, prog_cnt, lane);
+    if constexpr (kProg) flush_progress(p, prog_cur, prog_cnt, lane);
     if constexpr (kStats) {
         atomicAdd(p.stats + 0, (unsigned long long)st.segments);
         atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
@@ -1165,22 +1167,27 @@ hipError_t launch_to_srgba(const double* rgb, size_t n_pixels, uint32_t* rgba, c
 
 using KernelFn = void (*)(KernelParams);
 
-template <bool kBVH, bool kSpill, bool kStats>
+template <bool kBVH, bool kSpill, bool kStats, bool kProg>
 static KernelFn pick_kernel3(int lds_mode) {
-    if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill>;
+    if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill, kProg>;
     if constexpr (kBVH)
-        if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill>;
-    return render_kernel<0, kBVH, kStats, kSpill>;
+        if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill, kProg>;
+    return render_kernel<0, kBVH, kStats, kSpill, kProg>;
 }
 
+// Instrumentation: the stats instance counts segments and tests; the progress
+// instance feeds tray_render_progress; neither is ever timed by the bench.
 template <bool kBVH, bool kSpill>
-static KernelFn pick_kernel2(int lds_mode, bool stats) {
-    return stats ? pick_kernel3<kBVH, kSpill, true>(lds_mode) : pick_kernel3<kBVH, kSpill, false>(lds_mode);
+static KernelFn pick_kernel2(int lds_mode, bool stats, bool progress) {
+    if (stats) return pick_kernel3<kBVH, kSpill, true, false>(lds_mode);
+    if (progress) return pick_kernel3<kBVH, kSpill, false, true>(lds_mode);
+    return pick_kernel3<kBVH, kSpill, false, false>(lds_mode);
 }
 
-static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool spill) {
-    if (!bvh) return pick_kernel2<false, false>(lds_mode, stats);
-    return spill ? pick_kernel2<true, true>(lds_mode, stats) : pick_kernel2<true, false>(lds_mode, stats);
+static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, bool spill) {
+    if (!bvh) return pick_kernel2<false, false>(lds_mode, stats, progress);
+    return spill ? pick_kernel2<true, true>(lds_mode, stats, progress)
+                 : pick_kernel2<true, false>(lds_mode, stats, progress);
 }
 
 static KernelFn pick_resolve(int fmt) {
@@ -1312,7 +1319,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     }
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
-    const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, use_bvh && p.stack_cap > p.stack_lds);
+    const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr, use_bvh && p.stack_cap > p.stack_lds);
     const KernelFn resolve = pick_resolve(p.out_format);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {
