@@ -211,6 +211,18 @@ int tray_render_progress(const tray_sphere *spheres, int32_t n_spheres, const tr
                          const tray_camera *camera, const tray_params *params, int32_t device, void *out,
                          uint32_t *segments_out, tray_progress_fn progress, void *user);
 
+/* tray_render over several devices of this process (the one-process form of
+ * the multi-GPU row split): row y of the row set goes to devices[(y - y_start)
+ * % n_devices] (interleaved 1-row tiles, as bench.py --gpus N splits a frame),
+ * every device renders its rows concurrently, and the rows land in `out` in
+ * image order (compact from y_start, exactly as tray_render writes them). A
+ * device may be listed more than once (its shards render on separate streams).
+ * params->tile_rows must be 0. Bit-identical to tray_render for any list: every
+ * draw is keyed on the global pixel index. */
+int tray_render_devices(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
+                        const tray_camera *camera, const tray_params *params, const int32_t *devices,
+                        int32_t n_devices, void *out, uint32_t *segments_out);
+
 /* Device-resident scene for repeated renders (the scene is read-only during
  * Render, ray/tracer.go:48). */
 int tray_scene_upload(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,

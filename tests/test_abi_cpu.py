@@ -233,3 +233,20 @@ def test_srgb_threshold_encoding_equals_encoder(L, O):
     host = np.zeros((len(rgb), 4), dtype=np.uint8)
     L.check(L.lib().tray_to_srgba(rgb.ctypes.data, len(rgb), host.ctypes.data))
     assert np.array_equal(host, O.to_srgba(rgb))
+
+
+def test_render_devices_argument_checks(L):
+    s = L.spheres_array(None)
+    bg, cam = L.Background(), L.CameraState()
+    out = np.zeros(8 * 8 * 24, dtype=np.uint8)
+    devs = (ctypes.c_int32 * 2)(0, 0)
+    lib = L.lib()
+    p = L.make_params(8, 8, 5, 1, 0.5, 1)
+    assert lib.tray_render_devices(None, 0, ctypes.byref(bg), ctypes.byref(cam), ctypes.byref(p), devs, 0,
+                                   out.ctypes.data, None) == L.TRAY_ERR_INVALID_ARGUMENT
+    q = L.make_params(8, 8, 5, 1, 0.5, 1, tile_rows=1, tile_count=2)
+    assert lib.tray_render_devices(None, 0, ctypes.byref(bg), ctypes.byref(cam), ctypes.byref(q), devs, 2,
+                                   out.ctypes.data, None) == L.TRAY_ERR_INVALID_ARGUMENT
+    if not os.path.exists("/dev/kfd"):
+        assert lib.tray_render_devices(None, 0, ctypes.byref(bg), ctypes.byref(cam), ctypes.byref(p), devs, 2,
+                                       out.ctypes.data, None) == L.TRAY_ERR_NO_DEVICE

@@ -520,3 +520,23 @@ def test_hollow_glass_and_chunk_straddling_pixels(L, O, spp, radius):
     check(got, seg, ref, rseg)
     lin, sl = gpu_render(L, s, DEFAULT_BG, st, w, h, spp, 20, radius, 5, flags=L.FLAG_LINEAR_SCAN)
     assert np.array_equal(sl, seg) and np.array_equal(lin, got)
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_render_devices_equals_single_device(L, O, devices):
+    """tray_render_devices (the row split over several devices of one process; on
+    one GPU the shards repeat device 0 on separate streams) writes the same rows,
+    bytes and segment counts as tray_render, for every output format and for a
+    ragged row range."""
+    sc = O.rich_scene(2)
+    w, h = 70, 43
+    st = camera(L, RICH_SETUP, w, h)
+    bg = bg_struct(L, DEFAULT_BG)
+    for fmt in (L.OUT_RGB_F64, L.OUT_RGB_F32, L.OUT_RGBA8):
+        for y0, y1 in ((0, h), (5, 38)):
+            p = L.make_params(w, h, 20, 3, 0.5, 6, y_start=y0, y_end=y1, output=fmt)
+            one, s1 = L.render(sc, bg, st, p, 0, segments=True)
+            many, sm = L.render_devices(sc, bg, st, p, devices, segments=True)
+            assert np.array_equal(one, many) and np.array_equal(s1, sm), (fmt, y0, y1)
+    with pytest.raises(L.TrayError):  # it tiles rows itself
+        L.render_devices(sc, bg, st, L.make_params(w, h, 5, 1, 0.5, 1, tile_rows=2, tile_count=2), devices)

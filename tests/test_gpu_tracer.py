@@ -142,3 +142,22 @@ def test_progress_is_live(ray):  # tracer.go:126-128: ProgressFunc per row WHILE
     t.ProgressFunc = seen.append
     t.Render(ray.RichScene(2))
     assert seen == [64] * 36
+
+
+def test_tracer_devices_split_is_invisible(ray):
+    """Tracer.Devices (no Go counterpart): the frame's rows split over several
+    devices of one process (tray_render_devices) give the same image as one device."""
+    def render(devices):
+        t = ray.New(48, 27)
+        t.Camera = ray.RichSceneCamera()
+        t.MaxDepth, t.NumRaysPerPixel, t.Seed = 20, 4, 3
+        t.Devices = devices
+        rows = []
+        t.ProgressFunc = rows.append
+        img = t.Render(ray.RichScene(2)).copy()
+        assert rows == [48] * 27
+        return img, t.linear.copy()
+
+    a, la = render(None)
+    b, lb = render([0, 0, 0])
+    assert np.array_equal(a, b) and np.array_equal(la, lb)

@@ -128,6 +128,7 @@ EXPORTS = (
     "tray_rich_scene_capacity",
     "tray_render",
     "tray_render_progress",
+    "tray_render_devices",
     "tray_scene_upload",
     "tray_scene_release",
     "tray_scene_get_info",
@@ -172,6 +173,9 @@ def lib(path: str | None = None) -> ctypes.CDLL:
                               ctypes.POINTER(Params), i32, vp, u32p]
     if hasattr(L, "tray_render_progress"):  # absent from older builds (A/B tools)
         L.tray_render_progress.argtypes = L.tray_render.argtypes + [PROGRESS_FN, vp]
+    if hasattr(L, "tray_render_devices"):
+        L.tray_render_devices.argtypes = [vp, i32, ctypes.POINTER(Background), ctypes.POINTER(CameraState),
+                                          ctypes.POINTER(Params), ctypes.POINTER(i32), i32, vp, u32p]
     if hasattr(L, "tray_linear_to_srgba_async"):
         L.tray_linear_to_srgba_async.argtypes = [vp, ctypes.c_size_t, vp, i32, vp]
     L.tray_scene_upload.argtypes = [vp, i32, ctypes.POINTER(Background), i32, ctypes.POINTER(vp)]
@@ -238,6 +242,23 @@ def render(spheres, background: Background, camera: CameraState, params: Params,
     else:
         cb = PROGRESS_FN(lambda rows, _user: progress(int(rows)))  # kept alive for the call
         check(lib().tray_render_progress(*args, cb, None))
+    return out, seg
+
+
+def render_devices(spheres, background: Background, camera: CameraState, params: Params, devices,
+                   segments: bool = False):
+    """tray_render_devices: the row set split over `devices` (interleaved 1-row
+    tiles, a device may repeat), rows returned in image order like render()."""
+    s = spheres_array(spheres)
+    rows = params_rows(params)
+    ch = 4 if params.output == OUT_RGBA8 else 3
+    dtype = {OUT_RGB_F64: np.float64, OUT_RGB_F32: np.float32, OUT_RGBA8: np.uint8}[params.output]
+    out = np.zeros((rows, params.width, ch), dtype=dtype)
+    seg = np.zeros((rows, params.width), dtype=np.uint32) if segments else None
+    devs = (ctypes.c_int32 * len(devices))(*devices)
+    check(lib().tray_render_devices(s.ctypes.data if len(s) else None, len(s), ctypes.byref(background),
+                                    ctypes.byref(camera), ctypes.byref(params), devs, len(devices), out.ctypes.data,
+                                    seg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) if seg is not None else None))
     return out, seg
 
 

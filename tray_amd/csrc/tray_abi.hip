@@ -41,26 +41,37 @@ static int hip_fail(hipError_t e, const char* what) {
         if (e_ != hipSuccess) return hip_fail(e_, #call); \
     } while (0)
 
-// Per-device state of the synchronous entry points (tray_render*): their
-// stream and workspaces, the last scene they uploaded (reused while a caller
-// renders the same scene again, as main.go does on every resize), the progress
-// counters, and the sRGB encoder table of tray_linear_to_srgba_async.
-struct DeviceState {
-    std::mutex mu;
-    bool checked = false;
-    bool usable = false;
+// One render slot of a device for the synchronous entry points: a stream, the
+// output workspaces, and the last scene the slot uploaded (reused while the
+// caller passes the same scene again, as main.go does on every resize).
+// tray_render uses slot 0; tray_render_devices uses slot j for the j-th time a
+// device appears in its list (each slot's renders are ordered on its stream).
+struct Slot {
     hipStream_t stream = nullptr;
     void* out_ws = nullptr;
     size_t out_ws_bytes = 0;
     uint32_t* seg_ws = nullptr;
     size_t seg_ws_bytes = 0;
+    tray_scene_s* cached = nullptr;
+    std::vector<tray_sphere> cached_spheres;
+    tray_background cached_bg;
+};
+
+// Per-device state: render slots, the progress counters and the sRGB encoder
+// table of tray_linear_to_srgba_async.
+struct DeviceState {
+    std::mutex mu;
+    bool checked = false;
+    bool usable = false;
+    std::vector<Slot> slots;
     uint32_t* prog_host = nullptr;  // samples finished per 8-row tile row (host-mapped, coherent)
     uint32_t* prog_dev = nullptr;   // its device address
     size_t prog_bytes = 0;
     double* srgb = nullptr;         // tray::srgb_thresholds on the device
-    tray_scene_s* cached = nullptr;  // the scene of the last tray_render call
-    std::vector<tray_sphere> cached_spheres;
-    tray_background cached_bg;
+    Slot& slot(size_t j) {
+        if (slots.size() <= j) slots.resize(j + 1);
+        return slots[j];
+    }
 };
 
 static std::mutex g_devices_mu;
@@ -491,28 +502,37 @@ static hipError_t grow(void** buf, size_t* have, size_t bytes) {
     return e;
 }
 
-// The scene of a tray_render* call: the device's cached upload when the caller
-// passes the same spheres and background as last time (compared byte for byte;
-// the caller's arrays are copied, never retained), else a fresh upload that
-// replaces it. Called with st->mu held.
-static int cached_scene(DeviceState* st, const tray_sphere* spheres, int32_t n, const tray_background* bg,
-                        int32_t device, tray_scene_t* out) {
-    const bool same = st->cached && (int32_t)st->cached_spheres.size() == n &&
-                      (n == 0 || memcmp(st->cached_spheres.data(), spheres, sizeof(tray_sphere) * (size_t)n) == 0) &&
-                      memcmp(&st->cached_bg, bg, sizeof(*bg)) == 0;
+// The scene of a slot: its cached upload when the caller passes the same
+// spheres and background as last time (compared byte for byte; the caller's
+// arrays are copied, never retained), else a fresh upload that replaces it.
+// Called with the device's mutex held.
+static int cached_scene(Slot& sl, const tray_sphere* spheres, int32_t n, const tray_background* bg, int32_t device,
+                        tray_scene_t* out) {
+    const bool same = sl.cached && (int32_t)sl.cached_spheres.size() == n &&
+                      (n == 0 || memcmp(sl.cached_spheres.data(), spheres, sizeof(tray_sphere) * (size_t)n) == 0) &&
+                      memcmp(&sl.cached_bg, bg, sizeof(*bg)) == 0;
     if (!same) {
-        if (st->cached) tray_scene_release(st->cached);
-        st->cached = nullptr;
-        st->cached_spheres.clear();
+        if (sl.cached) tray_scene_release(sl.cached);
+        sl.cached = nullptr;
+        sl.cached_spheres.clear();
         tray_scene_t sc = nullptr;
         const int rc = tray_scene_upload(spheres, n, bg, device, &sc);
         if (rc) return rc;
-        st->cached = sc;
-        if (n > 0) st->cached_spheres.assign(spheres, spheres + n);
-        st->cached_bg = *bg;
+        sl.cached = sc;
+        if (n > 0) sl.cached_spheres.assign(spheres, spheres + n);
+        sl.cached_bg = *bg;
     }
-    *out = st->cached;
+    *out = sl.cached;
     return TRAY_OK;
+}
+
+// Stream and output workspaces of a slot for `npix` pixels.
+static hipError_t prepare_slot(Slot& sl, size_t out_bytes, size_t seg_bytes) {
+    hipError_t e = hipSuccess;
+    if (!sl.stream) e = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = grow(&sl.out_ws, &sl.out_ws_bytes, out_bytes);
+    if (e == hipSuccess && seg_bytes) e = grow(reinterpret_cast<void**>(&sl.seg_ws), &sl.seg_ws_bytes, seg_bytes);
+    return e;
 }
 
 int tray_render(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,
@@ -538,13 +558,12 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
     tray_scene_t sc = nullptr;
-    rc = cached_scene(st, spheres, n, bg, device, &sc);
+    Slot& sl = st->slot(0);
+    rc = cached_scene(sl, spheres, n, bg, device, &sc);
     if (rc) return rc;
-    if (!st->stream) e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
     const size_t out_bytes = npix * bytes_per_pixel(p->output);
-    if (e == hipSuccess) e = grow(&st->out_ws, &st->out_ws_bytes, out_bytes);
     const size_t seg_bytes = npix * sizeof(uint32_t);
-    if (e == hipSuccess && segments_out) e = grow(reinterpret_cast<void**>(&st->seg_ws), &st->seg_ws_bytes, seg_bytes);
+    e = prepare_slot(sl, out_bytes, segments_out ? seg_bytes : 0);
     // Progress: one counter of finished samples per 8-row tile row of the compact rows.
     const int32_t tile_rows = (rows + 7) / 8;
     const size_t prog_bytes = (size_t)tile_rows * sizeof(uint32_t);
@@ -561,7 +580,7 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
     }
     if (e == hipSuccess && progress) memset(st->prog_host, 0, prog_bytes);  // the stream is idle here
     if (e != hipSuccess) return hip_fail(e, "workspace");
-    rc = render_async_impl(sc, cam, p, st->out_ws, segments_out ? st->seg_ws : nullptr, nullptr, st->stream, 1,
+    rc = render_async_impl(sc, cam, p, sl.out_ws, segments_out ? sl.seg_ws : nullptr, nullptr, sl.stream, 1,
                            progress ? st->prog_dev : nullptr);
     if (rc) return rc;
     // Poll the counters while the launch runs and report the rows of every tile
@@ -572,7 +591,7 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
         const uint64_t per_row = (uint64_t)p->width * (uint64_t)p->rays_per_pixel;
         std::vector<uint8_t> done((size_t)tile_rows, 0);
         const volatile uint32_t* counts = st->prog_host;
-        while ((e = hipStreamQuery(st->stream)) == hipErrorNotReady) {
+        while ((e = hipStreamQuery(sl.stream)) == hipErrorNotReady) {
             std::this_thread::sleep_for(std::chrono::microseconds(500));
             int32_t fresh = 0;
             for (int32_t t = 0; t < tile_rows; ++t) {
@@ -589,13 +608,96 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
         }
         if (e != hipSuccess) return hip_fail(e, "render");
     }
-    e = hipMemcpyAsync(out, st->out_ws, out_bytes, hipMemcpyDeviceToHost, st->stream);
+    e = hipMemcpyAsync(out, sl.out_ws, out_bytes, hipMemcpyDeviceToHost, sl.stream);
     if (e == hipSuccess && segments_out)
-        e = hipMemcpyAsync(segments_out, st->seg_ws, seg_bytes, hipMemcpyDeviceToHost, st->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(st->stream);
+        e = hipMemcpyAsync(segments_out, sl.seg_ws, seg_bytes, hipMemcpyDeviceToHost, sl.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(sl.stream);
     if (e != hipSuccess) return hip_fail(e, "render");
     if (progress && reported < rows) progress(rows - reported, user);
     return TRAY_OK;
+}
+
+int tray_render_devices(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,
+                        const tray_params* p, const int32_t* devices, int32_t n_devices, void* out,
+                        uint32_t* segments_out) {
+    if (!bg || !cam || !out || !devices) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+    if (n_devices < 1 || n_devices > 1024) return fail(TRAY_ERR_INVALID_ARGUMENT, "n_devices must be in [1, 1024]");
+    int rc = validate_params(p);
+    if (rc) return rc;
+    if (p->tile_rows != 0) return fail(TRAY_ERR_INVALID_ARGUMENT, "tray_render_devices tiles the rows itself: tile_rows must be 0");
+    rc = validate_spheres(spheres, n);
+    if (rc) return rc;
+    // Every distinct device, locked in ascending order (no lock-order inversion between callers).
+    std::vector<int32_t> uniq(devices, devices + n_devices);
+    std::sort(uniq.begin(), uniq.end());
+    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+    std::vector<DeviceState*> states(uniq.size());
+    for (size_t i = 0; i < uniq.size(); ++i) {
+        rc = device_state(uniq[i], &states[i]);
+        if (rc) return rc;
+    }
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (DeviceState* st : states) locks.emplace_back(st->mu);
+    const int32_t rows = tray_params_rows(p);
+    if (rows == 0) return TRAY_OK;
+    const size_t row_bytes = (size_t)p->width * bytes_per_pixel(p->output);
+    const size_t seg_row_bytes = (size_t)p->width * sizeof(uint32_t);
+    struct Shard {
+        int32_t device;
+        Slot* slot;
+        tray_params params;
+        int32_t rows;
+    };
+    std::vector<Shard> shards((size_t)n_devices);
+    std::vector<int32_t> used(uniq.size(), 0);
+    hipError_t e = hipSuccess;
+    // Shard k renders the interleaved 1-row tiles k, k + n, ... of the row set
+    // (tile k -> shard k mod n), each on its own slot and stream.
+    for (int32_t k = 0; k < n_devices; ++k) {
+        const size_t u = (size_t)(std::lower_bound(uniq.begin(), uniq.end(), devices[k]) - uniq.begin());
+        Shard& sh = shards[(size_t)k];
+        sh.device = devices[k];
+        sh.slot = &states[u]->slot((size_t)used[u]++);
+        sh.params = *p;
+        sh.params.tile_rows = 1;
+        sh.params.tile_count = n_devices;
+        sh.params.tile_index = k;
+        sh.rows = tray_params_rows(&sh.params);
+        if (sh.rows == 0) continue;
+        e = hipSetDevice(sh.device);
+        if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+        tray_scene_t sc = nullptr;
+        rc = cached_scene(*sh.slot, spheres, n, bg, sh.device, &sc);
+        if (rc) return rc;
+        e = prepare_slot(*sh.slot, (size_t)sh.rows * row_bytes, segments_out ? (size_t)sh.rows * seg_row_bytes : 0);
+        if (e != hipSuccess) return hip_fail(e, "workspace");
+        rc = render_async_impl(sc, cam, &sh.params, sh.slot->out_ws, segments_out ? sh.slot->seg_ws : nullptr, nullptr,
+                               sh.slot->stream);
+        if (rc) return rc;  // launches already enqueued on other slots finish on their own streams
+    }
+    // Every shard is rendering; scatter each shard's compact rows into image order
+    // (shard k's i-th row is row k + i * n of the row set) with one strided copy each.
+    for (int32_t k = 0; k < n_devices && e == hipSuccess; ++k) {
+        const Shard& sh = shards[(size_t)k];
+        if (sh.rows == 0) continue;
+        e = hipSetDevice(sh.device);
+        if (e == hipSuccess)
+            e = hipMemcpy2DAsync(static_cast<char*>(out) + (size_t)k * row_bytes, (size_t)n_devices * row_bytes,
+                                 sh.slot->out_ws, row_bytes, row_bytes, (size_t)sh.rows, hipMemcpyDeviceToHost,
+                                 sh.slot->stream);
+        if (e == hipSuccess && segments_out)
+            e = hipMemcpy2DAsync(segments_out + (size_t)k * p->width, (size_t)n_devices * seg_row_bytes,
+                                 sh.slot->seg_ws, seg_row_bytes, seg_row_bytes, (size_t)sh.rows,
+                                 hipMemcpyDeviceToHost, sh.slot->stream);
+    }
+    for (int32_t k = 0; k < n_devices; ++k) {  // drain every stream even after an error
+        const Shard& sh = shards[(size_t)k];
+        if (sh.rows == 0 || !sh.slot->stream) continue;
+        (void)hipSetDevice(sh.device);
+        const hipError_t s2 = hipStreamSynchronize(sh.slot->stream);
+        if (e == hipSuccess) e = s2;
+    }
+    return e == hipSuccess ? TRAY_OK : hip_fail(e, "render");
 }
 
 int tray_linear_to_srgba_async(const double* rgb_device, size_t n_pixels, uint8_t* rgba_device, int32_t device,
@@ -630,22 +732,20 @@ int tray_shutdown(void) {
         if (!st) continue;
         std::lock_guard<std::mutex> lk2(st->mu);
         (void)hipSetDevice((int)d);
-        if (st->stream) (void)hipStreamSynchronize(st->stream);
-        if (st->cached) tray_scene_release(st->cached);
-        if (st->out_ws) (void)hipFree(st->out_ws);
-        if (st->seg_ws) (void)hipFree(st->seg_ws);
+        for (Slot& sl : st->slots) {
+            if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+            if (sl.cached) tray_scene_release(sl.cached);
+            if (sl.out_ws) (void)hipFree(sl.out_ws);
+            if (sl.seg_ws) (void)hipFree(sl.seg_ws);
+            if (sl.stream) (void)hipStreamDestroy(sl.stream);
+        }
+        st->slots.clear();
         if (st->prog_host) (void)hipHostFree(st->prog_host);
         if (st->srgb) (void)hipFree(st->srgb);
-        if (st->stream) (void)hipStreamDestroy(st->stream);
-        st->cached = nullptr;
-        st->cached_spheres.clear();
-        st->out_ws = nullptr;
-        st->seg_ws = nullptr;
         st->prog_dev = nullptr;
         st->prog_host = nullptr;
         st->srgb = nullptr;
-        st->stream = nullptr;
-        st->out_ws_bytes = st->seg_ws_bytes = st->prog_bytes = 0;
+        st->prog_bytes = 0;
     }
     return TRAY_OK;
 }

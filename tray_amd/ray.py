@@ -210,6 +210,7 @@ class Tracer:  # ray/tracer.go:25-36
         self.ProgressFunc = None
         self.Seed = 0
         self.Device = 0  # which gfx950 device renders (no Go counterpart)
+        self.Devices = None  # several devices: rows split over them (tray_render_devices; no Go counterpart)
         self.width = width
         self.height = height
         self.imageData = np.zeros((height, width, 4), dtype=np.uint8)  # image.NewRGBA, tracer.go:43
@@ -261,8 +262,15 @@ class Tracer:  # ray/tracer.go:25-36
             def progress(rows):
                 for _ in range(rows):
                     self.ProgressFunc(self.width)
-        rgb, seg = _lib.render(scene.to_array(), _background(scene.Background), self.Camera._state, params,
-                               self.Device, segments=True, progress=progress)
+        if self.Devices and len(self.Devices) > 1:  # one process, several GPUs (progress after the render)
+            rgb, seg = _lib.render_devices(scene.to_array(), _background(scene.Background), self.Camera._state,
+                                           params, list(self.Devices), segments=True)
+            if progress is not None:
+                progress(y1 - y0)
+        else:
+            rgb, seg = _lib.render(scene.to_array(), _background(scene.Background), self.Camera._state, params,
+                                   self.Devices[0] if self.Devices else self.Device, segments=True,
+                                   progress=progress)
         self.linear[y0:y1] = rgb
         self.segments[y0:y1] = seg
         rgba = np.zeros((y1 - y0, self.width, 4), dtype=np.uint8)
