@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -63,7 +64,7 @@ struct DeviceState {
     std::mutex mu;
     bool checked = false;
     bool usable = false;
-    std::vector<Slot> slots;
+    std::deque<Slot> slots;  // a deque: growing it keeps references to existing slots valid
     uint32_t* prog_host = nullptr;  // samples finished per 8-row tile row (host-mapped, coherent)
     uint32_t* prog_dev = nullptr;   // its device address
     size_t prog_bytes = 0;
