@@ -186,7 +186,8 @@ int32_t tray_rich_scene_capacity(int32_t half_extent);
 
 /* ---- the hot path -------------------------------------------------------------- */
 /* Synchronous drop-in for Tracer.RenderLines (ray/tracer.go:120-155) over the
- * row set in *params: uploads the scene, renders on `device`, and copies the
+ * row set in *params: uploads the scene (or reuses the device's copy of the same
+ * scene, see tray_render_progress), renders on `device`, and copies the
  * compact rows into caller-owned host memory `out` (size: rows x width x
  * bytes-per-pixel of params->output). `segments_out` (nullable) receives the
  * per-pixel count of Scene.Hit calls summed over samples (uint32). */

@@ -540,3 +540,29 @@ def test_render_devices_equals_single_device(L, O, devices):
             assert np.array_equal(one, many) and np.array_equal(s1, sm), (fmt, y0, y1)
     with pytest.raises(L.TrayError):  # it tiles rows itself
         L.render_devices(sc, bg, st, L.make_params(w, h, 5, 1, 0.5, 1, tile_rows=2, tile_count=2), devices)
+
+
+def test_concurrent_synchronous_renders(L, O):
+    """The reference's Render is safe to call from several goroutines on distinct
+    tracers; so is tray_render from several threads (ctypes releases the GIL):
+    calls on one device serialise on its lock and every result equals the
+    sequential one, including when the threads alternate between two scenes
+    (the device's cached upload is replaced under the lock)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    scenes = [O.rich_scene(2), O.rich_scene(3)]
+    w, h = 40, 24
+    st = camera(L, RICH_SETUP, w, h)
+    bg = bg_struct(L, DEFAULT_BG)
+    jobs = [(k % 2, 3 + k) for k in range(12)]
+
+    def run(job):
+        sc, seed = job
+        p = L.make_params(w, h, 20, 2, 0.5, seed)
+        return L.render(scenes[sc], bg, st, p, 0, segments=True)
+
+    seq = [run(j) for j in jobs]
+    with ThreadPoolExecutor(6) as ex:
+        par = list(ex.map(run, jobs))
+    for (a, sa), (b, sb) in zip(seq, par):
+        assert np.array_equal(a, b) and np.array_equal(sa, sb)
