@@ -583,7 +583,10 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
     if (e != hipSuccess) return hip_fail(e, "workspace");
     rc = render_async_impl(sc, cam, p, sl.out_ws, segments_out ? sl.seg_ws : nullptr, nullptr, sl.stream, 1,
                            progress ? st->prog_dev : nullptr);
-    if (rc) return rc;
+    if (rc) {  // a band may already be enqueued: let it finish before the slot can be reused
+        (void)hipStreamSynchronize(sl.stream);
+        return rc;
+    }
     // Poll the counters while the launch runs and report the rows of every tile
     // row whose samples have all finished (ProgressFunc, ray/tracer.go:126-128).
     // Before the copies: a copy into pageable caller memory returns only once done.
@@ -674,7 +677,14 @@ int tray_render_devices(const tray_sphere* spheres, int32_t n, const tray_backgr
         if (e != hipSuccess) return hip_fail(e, "workspace");
         rc = render_async_impl(sc, cam, &sh.params, sh.slot->out_ws, segments_out ? sh.slot->seg_ws : nullptr, nullptr,
                                sh.slot->stream);
-        if (rc) return rc;  // launches already enqueued on other slots finish on their own streams
+        if (rc) {  // let what is already enqueued finish before the slots can be reused
+            for (int32_t j = 0; j <= k; ++j)
+                if (shards[(size_t)j].rows > 0 && shards[(size_t)j].slot->stream) {
+                    (void)hipSetDevice(shards[(size_t)j].device);
+                    (void)hipStreamSynchronize(shards[(size_t)j].slot->stream);
+                }
+            return rc;
+        }
     }
     // Every shard is rendering; scatter each shard's compact rows into image order
     // (shard k's i-th row is row k + i * n of the row set) with one strided copy each.
