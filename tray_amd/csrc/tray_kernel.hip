@@ -1102,32 +1102,10 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 // (the megakernel has finished with it), so no memset launch sits between
 // consecutive frames.
 // blockIdx.y is the pass within the launch.
+// The mean of a pixel's samples written in the output format (pixel `off` of pass `pass`).
 template <int kFmt>
-__global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
-    __shared__ double srgb[256];
-    if constexpr (kFmt == kOutRGBA8) {  // the encoder table, one entry per thread
-        srgb[threadIdx.x] = p.srgb[threadIdx.x];
-        __syncthreads();
-    }
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q == 0 && blockIdx.y == 0) *p.queue = 0u;
-    if (q >= p.frame_items / (uint32_t)p.spp) return;
-    const uint32_t item0 = blockIdx.y * p.frame_items + q * (uint32_t)p.spp;
-    int32_t x, j;
-    uint32_t s0, pass;
-    if (!decode_item(p, item0, x, j, s0, pass)) return;
-    const double* smp = p.samples + (size_t)item0 * 3;
-    D3 sum = d3(0, 0, 0);
-    // Loads of 8 samples are issued together; the adds stay in sample order.
-    int32_t s = 0;
-    for (; s + 8 <= p.spp; s += 8) {
-        double v[24];
-#pragma unroll
-        for (int k = 0; k < 24; ++k) v[k] = smp[3 * s + k];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sum = add(sum, d3(v[3 * k], v[3 * k + 1], v[3 * k + 2]));
-    }
-    for (; s < p.spp; ++s) sum = add(sum, d3(smp[3 * s], smp[3 * s + 1], smp[3 * s + 2]));
+__device__ __forceinline__ void write_mean(const KernelParams& p, const double* srgb, D3 sum, int32_t x, int32_t j,
+                                           uint32_t pass) {
     const double inv = 1.0 / (double)p.spp;  // colorSumDiv (ray/tracer.go:123)
     const D3 mean = smul(sum, inv);
     const size_t off = (size_t)j * (size_t)p.width + (size_t)x;
@@ -1145,6 +1123,72 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
     } else {
         static_cast<uint32_t*>(out)[off] = srgba_word(srgb, mean.x, mean.y, mean.z);
     }
+}
+
+// Staged resolve (rays per pixel a multiple of 8): a wave's 64 pixels are
+// consecutive work items, so their samples are one contiguous region of the
+// sample buffer. The wave copies each 8-sample slab of its 64 pixels (64 x 192 B)
+// into LDS with 16-byte loads that walk the region in address order (about 6
+// pixels per load instruction instead of 64 lines, one per lane), then every
+// lane adds its pixel's 8 samples from LDS in sample order.
+constexpr int kStageStride = 25;  // doubles per pixel slab in LDS: 24 + 1 of padding (bank spread)
+
+template <int kFmt, bool kStaged>
+__global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
+    __shared__ double srgb[256];
+    if constexpr (kFmt == kOutRGBA8) {  // the encoder table, one entry per thread
+        srgb[threadIdx.x] = p.srgb[threadIdx.x];
+        __syncthreads();
+    }
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q == 0 && blockIdx.y == 0) *p.queue = 0u;
+    const uint32_t npix = p.frame_items / (uint32_t)p.spp;  // a multiple of 64: waves are whole
+    if (q >= npix) return;
+    const uint32_t item0 = blockIdx.y * p.frame_items + q * (uint32_t)p.spp;
+    int32_t x, j;
+    uint32_t s0, pass;
+    const bool valid = decode_item(p, item0, x, j, s0, pass);
+    D3 sum = d3(0, 0, 0);
+    if constexpr (kStaged) {
+        __shared__ double stage[4][64 * kStageStride];
+        const uint32_t lane = threadIdx.x & 63u;
+        double* st = stage[threadIdx.x >> 6];
+        const uint32_t q0 = q - lane;  // the wave's first pixel
+        const double* base = p.samples + ((size_t)blockIdx.y * p.frame_items + (size_t)q0 * (uint32_t)p.spp) * 3;
+        for (int32_t s = 0; s < p.spp; s += 8) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {  // 768 16-B pieces: pixel t / 12, piece t % 12 of its 192-B slab
+                const uint32_t t = (uint32_t)k * 64u + lane;
+                const uint32_t i = t / 12u, c = t - i * 12u;
+                const double2 v = *reinterpret_cast<const double2*>(base + ((size_t)i * (uint32_t)p.spp + s) * 3 + 2 * c);
+                st[i * kStageStride + 2 * c] = v.x;
+                st[i * kStageStride + 2 * c + 1] = v.y;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const double* mine = st + lane * kStageStride;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sum = add(sum, d3(mine[3 * k], mine[3 * k + 1], mine[3 * k + 2]));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // every lane has read the slab before it is overwritten
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    } else {
+        if (!valid) return;
+        const double* smp = p.samples + (size_t)item0 * 3;
+        // Loads of 8 samples are issued together; the adds stay in sample order.
+        int32_t s = 0;
+        for (; s + 8 <= p.spp; s += 8) {
+            double v[24];
+#pragma unroll
+            for (int k = 0; k < 24; ++k) v[k] = smp[3 * s + k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sum = add(sum, d3(v[3 * k], v[3 * k + 1], v[3 * k + 2]));
+        }
+        for (; s < p.spp; ++s) sum = add(sum, d3(smp[3 * s], smp[3 * s + 1], smp[3 * s + 2]));
+    }
+    if (valid) write_mean<kFmt>(p, srgb, sum, x, j, pass);
 }
 
 // ColorF.ToSRGBA over a device buffer of linear colours (tray_linear_to_srgba_async).
@@ -1190,10 +1234,18 @@ static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, b
                  : pick_kernel2<true, false>(lds_mode, stats, progress);
 }
 
-static KernelFn pick_resolve(int fmt) {
-    if (fmt == kOutRGBF64) return resolve_kernel<kOutRGBF64>;
-    if (fmt == kOutRGBF32) return resolve_kernel<kOutRGBF32>;
-    return resolve_kernel<kOutRGBA8>;
+template <bool kStaged>
+static KernelFn pick_resolve2(int fmt) {
+    if (fmt == kOutRGBF64) return resolve_kernel<kOutRGBF64, kStaged>;
+    if (fmt == kOutRGBF32) return resolve_kernel<kOutRGBF32, kStaged>;
+    return resolve_kernel<kOutRGBA8, kStaged>;
+}
+
+// The staged resolve needs 8 | rays per pixel (whole 8-sample slabs).
+static KernelFn pick_resolve(int fmt, int32_t spp) {
+    bool staged = spp % 8 == 0;
+    if (const char* e = getenv("TRAY_RESOLVE_STAGED")) staged = staged && atoi(e) != 0;  // A/B
+    return staged ? pick_resolve2<true>(fmt) : pick_resolve2<false>(fmt);
 }
 
 // Blocks the device keeps resident for this kernel and LDS size (persistent grid cap).
@@ -1320,7 +1372,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
     const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr, use_bvh && p.stack_cap > p.stack_lds);
-    const KernelFn resolve = pick_resolve(p.out_format);
+    const KernelFn resolve = pick_resolve(p.out_format, p.spp);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {
         int dev;
