@@ -24,7 +24,7 @@ def main():
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"]
             # the timed kernel: render_kernel<mode, true, false (no stats), spill>
-            if "render_kernel" not in name or ", true, false," not in name or not name.endswith("false>(tray::KernelParams)"):
+            if "render_kernel<" not in name or "<1, true, false, false, false>" not in name:  # the timed BVH kernel
                 continue
             kernel = name
             key = (row["Counter_Name"], row["Dispatch_Id"])
