@@ -26,6 +26,14 @@ def _ensure_built():
 
 _ensure_built()
 
+# torch ships its own HIP runtime. If libtray_amd.so (linked against /opt/rocm's)
+# initialises HIP first in a process, torch then finds no GPU; loading torch
+# first makes both share torch's runtime. GPU tests use torch for device buffers.
+try:
+    import torch  # noqa: F401
+except ImportError:  # the CPU suite does not need it
+    pass
+
 
 @pytest.fixture(scope="session")
 def O():

@@ -266,7 +266,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         for (int leaf_max = leaf_lo; leaf_max <= leaf_hi; leaf_max *= 2) {
             Bvh b;
             if (!build_bvh(spheres, n, &b, leaf_max)) continue;
-            const int32_t cap = b.stack_max + 1;  // + the scratch slot (tray_kernel.hip Stack)
+            const int32_t cap = b.stack_max + kStackSlack;  // + scratch slots (tray_kernel.hpp)
             if (bvh_scene_lds_bytes(0, 0, 0, cap) > kMaxLDSBytes) continue;  // stack alone too deep
             const int r = bvh_lds_plan((int32_t)b.nodes.size(), (int32_t)b.geo.size(), (int32_t)b.leaves.size(), cap).rank;
             if (r > rank) {
@@ -286,7 +286,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->n_leaves = (int32_t)bvh.leaves.size();
     sc->leaves = nullptr;
     sc->stack_ovf = nullptr;
-    sc->stack_cap = bvh.stack_max + 1;
+    sc->stack_cap = bvh.stack_max + kStackSlack;
     sc->leaf_max = has_bvh ? bvh.leaf_max : 0;
     sc->n_global = has_bvh ? bvh.n_global : 0;
     sc->nodes = nullptr;
@@ -319,7 +319,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
     if (e == hipSuccess && has_bvh) {
         e = hipMalloc(&sc->nodes, sizeof(Bvh4Node) * bvh.nodes.size());
-        const size_t ovf = bvh_stack_overflow_bytes(bvh.stack_max + 1, device);
+        const size_t ovf = bvh_stack_overflow_bytes(bvh.stack_max + kStackSlack, device);
         if (e == hipSuccess && ovf) e = hipMalloc(&sc->stack_ovf, ovf);
         if (e == hipSuccess) e = hipMalloc(&sc->leaves, sizeof(int32_t) * bvh.leaves.size());
         if (e == hipSuccess)
@@ -362,7 +362,7 @@ int tray_scene_get_info(tray_scene_t sc, tray_scene_info* out) {
     out->leaf_max = sc->leaf_max;
     out->n_nodes = sc->n_nodes;
     out->n_leaves = sc->n_leaves;
-    out->stack_depth = sc->has_bvh ? sc->stack_cap - 1 : 0;
+    out->stack_depth = sc->has_bvh ? sc->stack_cap - kStackSlack : 0;
     out->lds_resident = sc->has_bvh ? bvh_lds_plan(sc->n_nodes, sc->n_slots, sc->n_leaves, sc->stack_cap).mode : 0;
     out->n_global = sc->n_global;
     out->bound = sc->bvh_bound;

@@ -33,6 +33,7 @@
 #include <algorithm>
 
 #include "bvh.hpp"
+#include "fp64.hpp"
 #include "rng.hpp"
 #include "tray_kernel.hpp"
 
@@ -85,8 +86,8 @@ __device__ __forceinline__ double length_sq(D3 v) { return v.x * v.x + v.y * v.y
 // Unit (ray/vec3.go:116-119): each component divided by the length. `lsq` is
 // length_sq(v) when the caller already has it (same bits).
 __device__ __forceinline__ D3 unit_lsq(D3 v, double lsq) {
-    const double l = __builtin_sqrt(lsq);
-    return sdiv_rcp(v, l, 1.0 / l);
+    const double l = sqrt_cr(lsq);
+    return sdiv_rcp(v, l, rcp_cr(l));
 }
 __device__ __forceinline__ D3 unit(D3 v) { return unit_lsq(v, length_sq(v)); }
 __device__ __forceinline__ bool near_zero(D3 v) {
@@ -100,7 +101,7 @@ __device__ __forceinline__ D3 reflect(D3 v, D3 n) { return sub(v, smul(n, 2 * do
 __device__ __forceinline__ D3 refract(D3 uv, D3 n, double eta) {
     const double cos_theta = go_min1(dot(neg(uv), n));
     const D3 perp = smul(add(uv, smul(n, cos_theta)), eta);
-    const D3 par = smul(n, -__builtin_sqrt(__builtin_fabs(1.0 - length_sq(perp))));
+    const D3 par = smul(n, -sqrt_cr(__builtin_fabs(1.0 - length_sq(perp))));
     return add(perp, par);
 }
 // Reflectance (ray/materials.go:66-71) given r0 = ((1 - ref_idx) / (1 + ref_idx))^2,
@@ -115,7 +116,9 @@ __device__ __forceinline__ double reflectance(double cosine, double r0) {
 // InDisc(radius) (ray/tracer.go:138, ray/camera.go:128): polar map of two
 // uniforms: r = sqrt(ua), phi = 2 pi ub.
 __device__ __forceinline__ void disc(double ua, double ub, double radius, double& ox, double& oy) {
-    const double r = __builtin_sqrt(ua);
+    // ua = k 2^-32: 0 or >= 2^-32, inside sqrt_core's range
+    double r = sqrt_core(ua);
+    if (ua == 0) r = ua;
     double s, c;
     sincos_2pi(ub, s, c);
     ox = (r * c) * radius;
@@ -231,7 +234,7 @@ struct Lane {
 __device__ __forceinline__ void candidate(double h, double disc, double a, double a_inv, int idx, double& closest,
                                           int& best) {
     if (disc >= 0) {
-        const double sq = __builtin_sqrt(disc);
+        const double sq = sqrt_cr(disc);
         double root = div_rcp(h - sq, a, a_inv);
         bool ok = root > 1e-6 && root < closest;
         if (!ok) {
@@ -253,7 +256,7 @@ __device__ __forceinline__ void candidate(double h, double disc, double a, doubl
 __device__ __forceinline__ void candidate_any_order(double h, double disc, double a, double a_inv, int idx,
                                                     double& closest, int& best) {
     if (disc >= 0) {
-        const double sq = __builtin_sqrt(disc);
+        const double sq = sqrt_cr(disc);
         const double r1 = div_rcp(h - sq, a, a_inv);
         const double t = r1 > 1e-6 ? r1 : div_rcp(h + sq, a, a_inv);
         if (t > 1e-6 && (t < closest || (t == closest && idx < best))) {
@@ -282,6 +285,9 @@ __device__ __forceinline__ void quad(const double4 g, const D3& org, const D3& d
 #ifndef TRAY_PROFILE
 struct Stats {
     uint64_t segments = 0, spheres = 0, boxes = 0;
+#ifdef TRAY_STATS_PRIMARY  // diagnostic: node visits, leaf visits, box tests of primary segments; all node/leaf visits
+    uint64_t nodes0 = 0, leaves0 = 0, boxes0 = 0, nodes = 0, leaves = 0;
+#endif
 };
 #else  // phase profiles count in LDS; per-lane counters would cost registers
 struct NoCount {
@@ -315,7 +321,7 @@ template <int U, bool kStats>
 __device__ __forceinline__ int scene_hit_linear(const SceneView& sv, const D3& org, const D3& dir, double& closest,
                                                 Stats& st) {
     const double a = length_sq(dir);  // hoisted: same bits as per sphere
-    const double a_inv = 1.0 / a;
+    const double a_inv = rcp_cr(a);
     closest = __builtin_inf();
     int best = -1;
     const int ngroups = (sv.n + U - 1) / U;
@@ -348,8 +354,10 @@ __device__ __forceinline__ float f32_up(double v) {
 // (culled against the current closest hit), near-first descent with a per-lane
 // stack in LDS, FP64 sphere tests with the reference's arithmetic and the
 // any-order acceptance rule.
-// Lane states of the BVH kernel.
-enum : uint32_t { kIdleState = 0, kTravState = 1, kLeafState = 2, kShadeState = 3 };
+// Lane states of the BVH kernel, encoded in Trav::cur (no state register, no
+// per-step state bookkeeping): an inner node (< kBvhLeafBit) = traversing; a
+// leaf reference = waiting for the leaf phase; kBvhNone = traversal done,
+// waiting for the shade phase (busy lane) or idle (Lane::busy false).
 
 struct Trav {
     float ix, iy, iz, oix, oiy, oiz;  // FP32 ray: t = box * inv - org * inv
@@ -374,7 +382,7 @@ constexpr size_t kStackSlotBytes = (size_t)kBvhBlock * sizeof(uint32_t);
 
 // Per-lane traversal stack of sort keys. The top entry lives in Trav::top and
 // slot i >= 1 holds the entry below the i-th; slot 0 is a scratch slot, so
-// pushes need no branches (stack_cap = depth bound + 1). Slots below `lds`
+// pushes need no branches (stack_cap = depth bound + kStackSlack). Slots below `lds`
 // are in LDS, slot i of the lane at base[i * kBvhBlock] (consecutive lanes,
 // consecutive banks); a scene whose bound is deeper keeps the rest in a global
 // overflow area (spill set: one wave-uniform branch per access otherwise).
@@ -410,18 +418,17 @@ __device__ __forceinline__ void stack_store(const Stk& S, int32_t i, uint32_t v)
 // over its 16-bit reference. ~0 = no entry.
 __device__ __forceinline__ float key_tn(uint32_t key) { return __uint_as_float(key & 0xFFFF0000u); }
 
-__device__ __forceinline__ uint32_t state_of(uint32_t ref) {
-    return ref == kBvhNone ? kShadeState : (ref & kBvhLeafBit) ? kLeafState : kTravState;
-}
+__device__ __forceinline__ bool is_trav(uint32_t cur) { return cur < kBvhLeafBit; }
+__device__ __forceinline__ bool is_leaf(uint32_t cur) { return cur - kBvhLeafBit < kBvhNone - kBvhLeafBit; }
 
 __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& sv, const D3& org, const D3& dir) {
     T.a = length_sq(dir);  // hoisted: same bits as per sphere
-    T.a_inv = 1.0 / T.a;
+    T.a_inv = rcp_cr(T.a);
     T.closest = __builtin_inf();
     T.best = -1;
     T.slot = 0;
     T.tlim = __builtin_inff();
-    T.cur = 0;  // the root
+    T.cur = sv.n_nodes > 0 ? 0u : kBvhNone;  // the root
     T.sp = 0;
     T.top = ~0u;
     float dxf = (float)dir.x, dyf = (float)dir.y, dzf = (float)dir.z;
@@ -488,10 +495,10 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t be
 
 
 // One node visit: test the four child boxes, visit the nearest hit child next
-// (an inner node or a leaf) and push the other hit children far-to-near.
-// Returns the new lane state.
+// (an inner node or a leaf) and push the other hit children far-to-near. T.cur
+// becomes the next reference (the lane's state).
 template <class Stk>
-__device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, const Stk& S, uint32_t& tested) {
+__device__ __forceinline__ void trav_node(Trav& T, const SceneView& sv, const Stk& S, uint32_t& tested) {
     constexpr int32_t kPlane = 4 * kBvhWidth;  // far plane block = near ^ kPlane
     const char* nb = reinterpret_cast<const char*>(sv.nodes + T.cur);
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for a pop
@@ -542,18 +549,29 @@ __device__ __forceinline__ uint32_t trav_node(Trav& T, const SceneView& sv, cons
     }
 #undef TRAY_CX
     if (key[0] != ~0u) {
+        if constexpr (kBvhWidth == 4 && !Stk::spill) {
+            // Branch-free push of the hit children key[1..m] (sorted: invalid keys
+            // ~0 come last) far-to-near: slots sp, sp+1, sp+2 are written
+            // unconditionally; those above the new top are scratch (kStackSlack).
+            const bool v1 = key[1] != ~0u, v2 = key[2] != ~0u, v3 = key[3] != ~0u;
+            stack_store(S, T.sp, T.top);
+            stack_store(S, T.sp + 1, v3 ? key[3] : key[2]);
+            stack_store(S, T.sp + 2, key[2]);
+            T.top = v1 ? key[1] : T.top;
+            T.sp += (int32_t)v1 + (int32_t)v2 + (int32_t)v3;
+        } else {
 #pragma unroll
-        for (int k = kBvhWidth - 1; k >= 1; --k) stack_push(T, S, key[k]);
+            for (int k = kBvhWidth - 1; k >= 1; --k) stack_push(T, S, key[k]);
+        }
         T.cur = key[0] & 0xFFFFu;
     } else {
         T.cur = stack_pop(T, S, below);
     }
-    return state_of(T.cur);
 }
 
 // Test the spheres of leaf T.cur (FP64, any-order rule), then pop the next entry.
 template <class Stk>
-__device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, const Stk& S, const D3& org,
+__device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const Stk& S, const D3& org,
                                               const D3& dir, uint32_t& tested) {
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for the pop
     // One sphere per leaf: the leaf index is its slot (no leaf-table round trip).
@@ -573,7 +591,6 @@ __device__ __forceinline__ uint32_t trav_leaf(Trav& T, const SceneView& sv, cons
     }
     T.tlim = f32_up(T.closest);
     T.cur = stack_pop(T, S, below);
-    return state_of(T.cur);
 }
 
 // Chunks (64 work items each) a workgroup takes from the global queue per atomic.
@@ -761,7 +778,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         // One sqrt serves RandomUnitVector's sqrt(1 - z^2) and Dielectric's sin_theta.
         const double cos_theta = go_min1(dot(neg(ud), normal));
         const double z = 1.0 - 2.0 * u.u0;
-        const double sq = __builtin_sqrt(dielectric ? 1.0 - cos_theta * cos_theta : 1.0 - z * z);
+        const double sq = sqrt_cr(dielectric ? 1.0 - cos_theta * cos_theta : 1.0 - z * z);
         D3 uv = d3(0, 0, 0);
         if (lambertian || (m.type == kMetal && m.param > 0.0)) uv = unit_vector_from(z, sq, u.u1);
         if (lambertian) {  // ray/materials.go:13-20
@@ -817,6 +834,24 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #ifndef TRAY_REFILL_BATCH
 #define TRAY_REFILL_BATCH 24
 #endif
+
+// Cost probes (diagnostic builds only, never timed as the product): N extra
+// independent VALU instructions in one phase, to measure what an instruction
+// there costs (tools/ab_bench.py A/B against the plain build).
+#define TRAY_PROBE_F32(n)                                                     \
+    {                                                                         \
+        _Pragma("unroll") for (int i_ = 0; i_ < (n); ++i_) {                  \
+            float t_;                                                         \
+            asm volatile("v_add_f32_e64 %0, 1.0, 1.0" : "=v"(t_));            \
+        }                                                                     \
+    }
+#define TRAY_PROBE_F64(n)                                                     \
+    {                                                                         \
+        _Pragma("unroll") for (int i_ = 0; i_ < (n); ++i_) {                  \
+            double t_;                                                        \
+            asm volatile("v_add_f64 %0, 1.0, 1.0" : "=v"(t_));                \
+        }                                                                     \
+    }
 
 // Diagnostic build only (-DTRAY_PROFILE): per-wave s_memtime stamps around each
 // phase of the BVH loop, plus phase and active-lane counts, added into
@@ -937,7 +972,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     L.busy = false;
     Stats st;
     Trav T;
-    uint32_t state = kIdleState;
+    T.cur = kBvhNone;  // idle
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
     bool exhausted = false;
     int32_t prog_cur = 0;  // live progress: the wave's current tile row and its unflushed count
@@ -989,12 +1024,14 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             int32_t x, j;
             uint32_t smp, pass;
             if (fresh_item < p.items && decode_item(p, fresh_item, x, j, smp, pass)) {
+#ifdef TRAY_PROBE_REFILL
+                TRAY_PROBE_F32(TRAY_PROBE_REFILL)
+#endif
                 start_sample(p, uni, L, fresh_item, x, j, (p.pass0 + pass) * (uint32_t)p.spp + smp);
                 if constexpr (kBVH) {
                     ++L.segments;
                     trav_begin(T, sv, L.org, L.dir);
                     if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
-                    state = sv.n_nodes > 0 ? kTravState : kShadeState;
                 }
             }
         }
@@ -1020,52 +1057,73 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 PROF_T0();
 #pragma unroll 1
                 for (int s = 0; s < TRAY_NODE_STEPS; ++s) {
-                    const uint64_t m = __ballot(state == kTravState);
+                    const uint64_t m = __ballot(is_trav(T.cur));
                     if (m == 0ull) break;
                     PROF_CNT(4, 1);
                     PROF_CNT(5, __popcll(m));
-                    PROF_CNT(11, __popcll(__ballot(state == kLeafState)));   // waiting for the leaf phase
-                    PROF_CNT(12, __popcll(__ballot(state == kShadeState)));  // waiting for the shade phase
-                    if (state == kTravState) {
+                    PROF_CNT(11, __popcll(__ballot(is_leaf(T.cur))));             // waiting for the leaf phase
+                    PROF_CNT(12, __popcll(__ballot(L.busy && T.cur == kBvhNone)));  // waiting for the shade phase
+                    if (is_trav(T.cur)) {
                         uint32_t tested;
-                        state = trav_node(T, sv, S, tested);
+#ifdef TRAY_PROBE_NODE
+                        TRAY_PROBE_F32(TRAY_PROBE_NODE)
+#endif
+                        trav_node(T, sv, S, tested);
                         if constexpr (kStats) st.boxes += tested;
+#if defined(TRAY_STATS_PRIMARY) && !defined(TRAY_PROFILE)
+                        if constexpr (kStats) {
+                            ++st.nodes;
+                            if (L.bounce == 0) ++st.nodes0, st.boxes0 += tested;
+                        }
+#endif
                     }
                 }
                 PROF_ADD(1);
             }
             // Leaf phase: FP64 sphere tests, batched.
-            const uint64_t m_leaf = __ballot(state == kLeafState);
+            const uint64_t m_leaf = __ballot(is_leaf(T.cur));
             if (m_leaf != 0ull &&
-                (__popcll(m_leaf) >= TRAY_LEAF_BATCH || __ballot(state == kTravState) == 0ull)) {
+                (__popcll(m_leaf) >= TRAY_LEAF_BATCH || __ballot(is_trav(T.cur)) == 0ull)) {
                 PROF_T0();
                 PROF_CNT(6, 1);
                 PROF_CNT(7, __popcll(m_leaf));
-                if (state == kLeafState) {
+                if (is_leaf(T.cur)) {
                     uint32_t tested;
-                    state = trav_leaf(T, sv, S, L.org, L.dir, tested);
+#ifdef TRAY_PROBE_LEAF
+                    TRAY_PROBE_F32(TRAY_PROBE_LEAF)
+#endif
+                    trav_leaf(T, sv, S, L.org, L.dir, tested);
                     if constexpr (kStats) st.spheres += tested;
+#if defined(TRAY_STATS_PRIMARY) && !defined(TRAY_PROFILE)
+                    if constexpr (kStats) {
+                        ++st.leaves;
+                        if (L.bounce == 0) ++st.leaves0;
+                    }
+#endif
                 }
                 PROF_ADD(2);
             }
             // Shading phase, batched.
-            const uint64_t m_shade = __ballot(state == kShadeState);
-            if (m_shade != 0ull && (__popcll(m_shade) >= TRAY_SHADE_BATCH ||
-                                    __ballot(state == kTravState || state == kLeafState) == 0ull)) {
+            const uint64_t m_shade = __ballot(L.busy && T.cur == kBvhNone);
+            if (m_shade != 0ull && (__popcll(m_shade) >= TRAY_SHADE_BATCH || __ballot(T.cur < kBvhNone) == 0ull)) {
                 PROF_T0();
                 PROF_CNT(8, 1);
                 PROF_CNT(9, __popcll(m_shade));
                 bool ended = false;
-                if (state == kShadeState) {
+                if (L.busy && T.cur == kBvhNone) {
+#ifdef TRAY_PROBE_SHADE
+                    TRAY_PROBE_F32(TRAY_PROBE_SHADE)
+#endif
+#ifdef TRAY_PROBE_SHADE64
+                    TRAY_PROBE_F64(TRAY_PROBE_SHADE64)
+#endif
                     if (shade_step<kStats>(p, uni, L, T.best, T.closest, T.a, [&] { return sv.bgeo[T.slot]; },
                                            [&] { return sv.bmat[T.slot]; }, st)) {
                         ++L.segments;
                         trav_begin(T, sv, L.org, L.dir);
                         if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
-                        state = sv.n_nodes > 0 ? kTravState : kShadeState;
                     } else {
-                        state = kIdleState;
-                        ended = true;
+                        ended = true;  // idle: T.cur stays kBvhNone, L.busy is false
                     }
                 }
                 if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
@@ -1078,6 +1136,13 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         atomicAdd(p.stats + 0, (unsigned long long)st.segments);
         atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
         atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
+#if defined(TRAY_STATS_PRIMARY) && !defined(TRAY_PROFILE)
+        atomicAdd(p.stats + 3, (unsigned long long)st.nodes0);
+        atomicAdd(p.stats + 4, (unsigned long long)st.leaves0);
+        atomicAdd(p.stats + 5, (unsigned long long)st.boxes0);
+        atomicAdd(p.stats + 6, (unsigned long long)st.nodes);
+        atomicAdd(p.stats + 7, (unsigned long long)st.leaves);
+#endif
     }
 #ifdef TRAY_PROFILE
     if (kStats && lane == 0) {
@@ -1396,6 +1461,8 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (stats) {
 #ifdef TRAY_PROFILE
         e = hipMemsetAsync(p.stats, 0, 19 * sizeof(unsigned long long), stream);
+#elif defined(TRAY_STATS_PRIMARY)
+        e = hipMemsetAsync(p.stats, 0, 8 * sizeof(unsigned long long), stream);
 #else
         e = hipMemsetAsync(p.stats, 0, 3 * sizeof(unsigned long long), stream);
 #endif

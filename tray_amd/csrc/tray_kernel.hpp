@@ -57,6 +57,11 @@ struct V3 {
     double x, y, z;
 };
 
+// Traversal stack slots per lane beyond the depth bound (Bvh::stack_max): slot
+// 0, the scratch slot of a push, and the two slots above the top that the
+// branch-free three-entry push writes unconditionally (tray_kernel.hip trav_node).
+constexpr int32_t kStackSlack = 3;
+
 struct KernelParams {
     const double4* geo;  // n_pad entries: n spheres, then NaN padding (never hit)
     const MatRec* mat;
@@ -82,7 +87,7 @@ struct KernelParams {
     const MatRec* bmat;     // shading record per slot
     int32_t n_nodes, n_slots, n_leaves;
     int32_t n_global;       // spheres tested before the tree: slots [n_slots - n_global, n_slots)
-    int32_t stack_cap;      // traversal stack slots per lane (Bvh::stack_max + 1)
+    int32_t stack_cap;      // traversal stack slots per lane (Bvh::stack_max + kStackSlack)
     int32_t stack_lds;      // slots kept in LDS (set by launch_render)
     uint32_t* stack_ovf;    // slots beyond the LDS ones, stride = grid lanes
     unsigned long long* stats;  // nullable: [segments, sphere tests, box tests]
