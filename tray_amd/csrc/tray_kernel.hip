@@ -477,8 +477,26 @@ __device__ __forceinline__ void stack_push(Trav& T, const Stk& S, uint32_t key) 
 // One cull at most and no further LDS round trip: an entry that is still
 // beyond tlim is visited anyway, which the box tests and the any-order rule
 // make harmless. Returns its reference, or kBvhNone.
+#ifndef TRAY_POP_SENTINEL
+#define TRAY_POP_SENTINEL 1
+#endif
 template <class Stk>
 __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t below) {
+#if TRAY_POP_SENTINEL
+    // Slot 0 always holds ~0 (written only by a push at depth 0, from the empty
+    // top), so an empty stack pops ~0: key_tn(~0) is NaN (never culled) and
+    // ~0 & 0xFFFF is kBvhNone. No emptiness branches: one divergent cull.
+    uint32_t key = T.top;
+    T.top = below;
+    T.sp = max(T.sp - 1, 0);
+    if (key_tn(key) > T.tlim) {
+        key = T.top;
+        T.sp = max(T.sp - 1, 0);
+        T.top = stack_load(S, T.sp);  // the entry of depth sp sits in slot sp
+        if (T.sp == 0 && key_tn(key) > T.tlim) key = ~0u;
+    }
+    return key & 0xFFFFu;
+#else
     if (T.sp == 0) return kBvhNone;
     uint32_t key = T.top;
     --T.sp;
@@ -491,6 +509,7 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t be
         if (T.sp == 0 && key_tn(key) > T.tlim) return kBvhNone;
     }
     return key & 0xFFFFu;
+#endif
 }
 
 
