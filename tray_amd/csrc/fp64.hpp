@@ -39,7 +39,7 @@ __device__ __forceinline__ bool sqrt_core_ok(double x) { return hi_word(x) - 0x1
 __device__ __forceinline__ double sqrt_cr(double x) {
     double g = sqrt_core(x);
     if (x == 0) g = x;
-    if (__builtin_expect(!(x == 0 || sqrt_core_ok(x)), 0)) g = __builtin_sqrt(x);
+    if (__builtin_expect(!((x == 0) | sqrt_core_ok(x)), 0)) g = __builtin_sqrt(x);
     return g;
 }
 __device__ __forceinline__ double rcp_core(double b) {

@@ -61,12 +61,21 @@ __device__ __forceinline__ D3 neg(D3 v) { return d3(-v.x, -v.y, -v.z); }
 // the overflow/underflow range (or non-finite operands) take the full division.
 // Branch-free form: `ok` is cleared when the quotient needs the full division
 // (the caller then redoes its divisions in one rarely taken branch).
+#ifndef TRAY_INT_RANGE
+#define TRAY_INT_RANGE 1
+#endif
 __device__ __forceinline__ double div_rcp_try(double a, double b, double y, bool& ok) {
     const double q = a * y;
     const double r = __builtin_fma(-b, q, a);
     const double q1 = __builtin_fma(r, y, q);
+#if TRAY_INT_RANGE
+    // |q| in [2^-960, 2^960): biased exponent 63..1982, tested on the high word
+    // (bitwise, so no branches; NaN and infinities fail).
+    ok = ok & ((a == 0) | (((hi_word(q) & 0x7FF00000u) - (63u << 20)) < (1920u << 20)));
+#else
     const double aq = __builtin_fabs(q);
     ok = ok && (a == 0 || (aq > 0x1p-960 && aq < 0x1p+960));
+#endif
     return a == 0 ? q : q1;
 }
 __device__ __forceinline__ double div_rcp(double a, double b, double y) {
@@ -768,6 +777,9 @@ __device__ __forceinline__ void count_progress(const KernelParams& p, bool ended
 // Written for a wave of lanes on different branches: the work several branches
 // need is done once, before them — the bounce's Philox block and the unit
 // direction (sky, Metal, Dielectric).
+#ifndef TRAY_EARLY_MAT
+#define TRAY_EARLY_MAT 1
+#endif
 template <bool kStats, typename GeoAt, typename MatAt>
 __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
                                            double dir_lsq, GeoAt geo_at, MatAt mat_at, Stats& st) {
@@ -776,6 +788,13 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     // (RayColor(depth 0) is black), so no scatter is computed for it.
     const bool last = L.bounce + 1u >= (uint32_t)p.max_depth;
     bool ends = !hit || last;
+#if TRAY_EARLY_MAT
+    // Issued first, for every lane (a miss reads a valid record it ignores), so
+    // the L2 round trip of the shading record overlaps the FP64 work below
+    // instead of starting after it inside the hit branch.
+    const double4 g = geo_at();
+    const MatRec m = mat_at();
+#endif
     const U4 u = philox_u4(uni_seed(uni), L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
     const D3 ud = unit_lsq(L.dir, dir_lsq);  // dir_lsq = length_sq(L.dir), the segment's `a`
     D3 color = d3(0, 0, 0);
@@ -784,8 +803,10 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         const D3 bg_a = d3(uni->bg_a.x, uni->bg_a.y, uni->bg_a.z), bg_b = d3(uni->bg_b.x, uni->bg_b.y, uni->bg_b.z);
         color = mul(L.thr, add(smul(bg_a, 1.0 - t), smul(bg_b, t)));
     } else if (!last) {
+#if !TRAY_EARLY_MAT
         const double4 g = geo_at();
         const MatRec m = mat_at();
+#endif
         const D3 point = add(L.org, smul(L.dir, closest));                             // Ray.At (ray/ray.go:23-25)
         const D3 outward = sdiv_rcp(sub(point, d3(g.x, g.y, g.z)), m.radius, m.rinv);  // ray/objects.go:100
         const bool front = dot(L.dir, outward) < 0;                                    // SetFaceNormal (:19-26)
@@ -1066,8 +1087,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 ++L.segments;
                 double closest;
                 const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
-                ended = !shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[best]; },
-                                            [&] { return p.mat[best]; }, st);
+                ended = !shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[max(best, 0)]; },
+                                            [&] { return p.mat[max(best, 0)]; }, st);
             }
             if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
         } else {
