@@ -114,4 +114,40 @@ __host__ __device__ __forceinline__ void sincos_2pi(double u, double& s, double&
     c = qq == 0 ? ck : qq == 1 ? -sk : qq == 2 ? -ck : sk;
 }
 
+// sincos_2pi(w * 2^-32) from the uniform's 32-bit word, with the FP64 front
+// end (4u, floor, reflection, conversion to float) done in integers: 4u =
+// w 2^-30, so the quadrant is w >> 30 and f = F 2^-30 with F = w mod 2^30;
+// the reflection 1 - f = (2^30 - F) 2^-30 is exact, and (float) of G 2^-30 is
+// RN32(G) 2^-30 (an exact power-of-two scaling). Every step is exact or the
+// same single rounding as sincos_2pi's, so the bits are identical for every w
+// (tools/sincos_check.hip compares all 2^32 words on the device).
+__host__ __device__ __forceinline__ void sincos_2pi_word(uint32_t w, double& s, double& c) {
+    const uint32_t F = w & 0x3FFFFFFFu;
+    const bool swap = F > 0x20000000u;
+    const float x = (float)(swap ? 0x40000000u - F : F) * 0x1p-30f;
+    const float t = x * 0x1.921fb6p+0f;  // RN32(pi/2)
+    const float t2 = t * t;
+    float sp = __builtin_fmaf(t2, 0x1.71de3ap-19f, -0x1.a01a02p-13f);
+    sp = __builtin_fmaf(sp, t2, 0x1.111112p-7f);
+    sp = __builtin_fmaf(sp, t2, -0x1.555556p-3f);
+    sp = __builtin_fmaf(sp, t2, 1.0f);
+    float sn = t * sp;
+    float cp = __builtin_fmaf(t2, -0x1.27e4fcp-22f, 0x1.a01a02p-16f);
+    cp = __builtin_fmaf(cp, t2, -0x1.6c16c2p-10f);
+    cp = __builtin_fmaf(cp, t2, 0x1.555556p-5f);
+    cp = __builtin_fmaf(cp, t2, -0.5f);
+    float cs = __builtin_fmaf(cp, t2, 1.0f);
+    if (swap) {
+        const float tmp = sn;
+        sn = cs;
+        cs = tmp;
+    }
+    const double sd = sn, cd = cs;
+    const double k = 1.5 - 0.5 * (sd * sd + cd * cd);
+    const double sk = sd * k, ck = cd * k;
+    const uint32_t qq = w >> 30;
+    s = qq == 0 ? sk : qq == 1 ? ck : qq == 2 ? -sk : -ck;
+    c = qq == 0 ? ck : qq == 1 ? -sk : qq == 2 ? -ck : sk;
+}
+
 }  // namespace tray

@@ -122,14 +122,18 @@ __device__ __forceinline__ double reflectance(double cosine, double r0) {
     return r0 + (1 - r0) * (x * x4);
 }
 
+// The uniform u = w 2^-32 of a 32-bit Philox word (include/tray.h).
+__device__ __forceinline__ double uniform(uint32_t w) { return (double)w * 0x1.0p-32; }
+
 // InDisc(radius) (ray/tracer.go:138, ray/camera.go:128): polar map of two
-// uniforms: r = sqrt(ua), phi = 2 pi ub.
-__device__ __forceinline__ void disc(double ua, double ub, double radius, double& ox, double& oy) {
+// uniforms: r = sqrt(ua), phi = 2 pi ub (ub given as its word).
+__device__ __forceinline__ void disc(uint32_t wa, uint32_t wb, double radius, double& ox, double& oy) {
     // ua = k 2^-32: 0 or >= 2^-32, inside sqrt_core's range
+    const double ua = uniform(wa);
     double r = sqrt_core(ua);
-    if (ua == 0) r = ua;
+    if (wa == 0) r = ua;
     double s, c;
-    sincos_2pi(ub, s, c);
+    sincos_2pi_word(wb, s, c);
     ox = (r * c) * radius;
     oy = (r * s) * radius;
 }
@@ -165,25 +169,25 @@ __device__ __forceinline__ D3 ld3(const volatile __attribute__((address_space(3)
 
 // RandomUnitVector (ray/rand.go:30-32): Archimedes' projection of two uniforms of
 // the bounce's scatter block, z = 1 - 2 u0, r = sqrt(1 - z*z), phi = 2 pi u1.
-__device__ __forceinline__ D3 unit_vector_from(double z, double r, double u1) {
+__device__ __forceinline__ D3 unit_vector_from(double z, double r, uint32_t w1) {
     double s, c;
-    sincos_2pi(u1, s, c);
+    sincos_2pi_word(w1, s, c);
     return d3(r * c, r * s, z);
 }
 
 // The sample's camera block (purpose 1): (pixel, sample, 0, 1<<24).
-__device__ __forceinline__ U4 camera_block(UniPtr uni, uint32_t pixel, uint32_t sample) {
-    return philox_u4(uni_seed(uni), pixel, sample, 0u, kPurposeCamera << 24);
+__device__ __forceinline__ Block camera_block(UniPtr uni, uint32_t pixel, uint32_t sample) {
+    return philox4x32_10(uni_seed(uni), pixel, sample, 0u, kPurposeCamera << 24);
 }
 
 // Camera.GetRay (ray/camera.go:113-142). The sample's camera block `u` feeds the
 // anti-aliasing disc (words 0,1; ray/tracer.go:136-139, only when r > 1) and the
 // lens disc (words 2,3, only when the aperture is open).
-__device__ __forceinline__ void get_ray(const KernelParams& p, UniPtr uni, const U4& u, double px, double py,
+__device__ __forceinline__ void get_ray(const KernelParams& p, UniPtr uni, const Block& u, double px, double py,
                                         D3& origin, D3& dir) {
     double ox = 0.0, oy = 0.0;
     const double aperture = uni->cam.aperture;
-    if (p.spp > 1) disc(u.u0, u.u1, uni->ray_radius, ox, oy);
+    if (p.spp > 1) disc(u.x0, u.x1, uni->ray_radius, ox, oy);
     const D3 pos = ld3(uni->cam.position);
     const D3 p00 = ld3(uni->cam.pixel00);
     const D3 pxv = ld3(uni->cam.pixel_x);
@@ -193,7 +197,7 @@ __device__ __forceinline__ void get_ray(const KernelParams& p, UniPtr uni, const
     dir = sub(sample_pt, pos);
     if (aperture > 0) {
         double dx, dy;
-        disc(u.u2, u.u3, 1.0, dx, dy);
+        disc(u.x2, u.x3, 1.0, dx, dy);
         const D3 du = ld3(uni->cam.defocus_u);
         const D3 dv = ld3(uni->cam.defocus_v);
         const D3 offset = add(smul(du, dx), smul(dv, dy));
@@ -795,7 +799,8 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     const double4 g = geo_at();
     const MatRec m = mat_at();
 #endif
-    const U4 u = philox_u4(uni_seed(uni), L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
+    const Block w = philox4x32_10(uni_seed(uni), L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
+    const double u0 = uniform(w.x0);
     const D3 ud = unit_lsq(L.dir, dir_lsq);  // dir_lsq = length_sq(L.dir), the segment's `a`
     D3 color = d3(0, 0, 0);
     if (!hit) {  // AmbientLight.Hit (ray/objects.go:68-73)
@@ -817,10 +822,10 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         const bool lambertian = m.type == kLambertian, dielectric = m.type == kDielectric;
         // One sqrt serves RandomUnitVector's sqrt(1 - z^2) and Dielectric's sin_theta.
         const double cos_theta = go_min1(dot(neg(ud), normal));
-        const double z = 1.0 - 2.0 * u.u0;
+        const double z = 1.0 - 2.0 * u0;
         const double sq = sqrt_cr(dielectric ? 1.0 - cos_theta * cos_theta : 1.0 - z * z);
         D3 uv = d3(0, 0, 0);
-        if (lambertian || (m.type == kMetal && m.param > 0.0)) uv = unit_vector_from(z, sq, u.u1);
+        if (lambertian || (m.type == kMetal && m.param > 0.0)) uv = unit_vector_from(z, sq, w.x1);
         if (lambertian) {  // ray/materials.go:13-20
             new_dir = add(normal, uv);
             if (near_zero(new_dir)) new_dir = normal;
@@ -834,7 +839,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
             const double ratio = front ? m.pinv : m.param;  // 1.0/RefIdx precomputed (same bits)
             const double sin_theta = sq;
             const double r0 = front ? m.albedo[0] : m.albedo[1];
-            const bool do_reflect = ratio * sin_theta > 1.0 || reflectance(cos_theta, r0) > u.u0;
+            const bool do_reflect = ratio * sin_theta > 1.0 || reflectance(cos_theta, r0) > u0;
             new_dir = do_reflect ? reflect(ud, normal) : refract(ud, normal, ratio);
         }
         if (scattered) {
@@ -1087,8 +1092,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 ++L.segments;
                 double closest;
                 const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
-                ended = !shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[max(best, 0)]; },
-                                            [&] { return p.mat[max(best, 0)]; }, st);
+                ended = !shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[max(best, 0)]; },  // NaN-padded: entry 0 exists
+                                            [&] { return best >= 0 ? p.mat[best] : MatRec{}; }, st);
             }
             if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
         } else {
