@@ -64,19 +64,21 @@ __device__ __forceinline__ D3 neg(D3 v) { return d3(-v.x, -v.y, -v.z); }
 #ifndef TRAY_INT_RANGE
 #define TRAY_INT_RANGE 1
 #endif
+
 __device__ __forceinline__ double div_rcp_try(double a, double b, double y, bool& ok) {
     const double q = a * y;
     const double r = __builtin_fma(-b, q, a);
     const double q1 = __builtin_fma(r, y, q);
+    const bool a0 = a == 0;
 #if TRAY_INT_RANGE
     // |q| in [2^-960, 2^960): biased exponent 63..1982, tested on the high word
     // (bitwise, so no branches; NaN and infinities fail).
-    ok = ok & ((a == 0) | (((hi_word(q) & 0x7FF00000u) - (63u << 20)) < (1920u << 20)));
+    ok = ok & (a0 | (((hi_word(q) & 0x7FF00000u) - (63u << 20)) < (1920u << 20)));
 #else
     const double aq = __builtin_fabs(q);
-    ok = ok && (a == 0 || (aq > 0x1p-960 && aq < 0x1p+960));
+    ok = ok && (a0 || (aq > 0x1p-960 && aq < 0x1p+960));
 #endif
-    return a == 0 ? q : q1;
+    return a0 ? q : q1;
 }
 __device__ __forceinline__ double div_rcp(double a, double b, double y) {
     bool ok = true;
@@ -434,6 +436,17 @@ __device__ __forceinline__ float key_tn(uint32_t key) { return __uint_as_float(k
 __device__ __forceinline__ bool is_trav(uint32_t cur) { return cur < kBvhLeafBit; }
 __device__ __forceinline__ bool is_leaf(uint32_t cur) { return cur - kBvhLeafBit < kBvhNone - kBvhLeafBit; }
 
+// Sphere.Hit of the sphere in leaf slot `slot` under the any-order rule.
+__device__ __forceinline__ void test_slot(Trav& T, const SceneView& sv, int32_t slot, const D3& org, const D3& dir) {
+    double h, d;
+    quad(sv.bgeo[slot], org, dir, T.a, h, d);
+    if (d >= 0) {
+        const int32_t before = T.best;
+        candidate_any_order(h, d, T.a, T.a_inv, sv.bidx[slot], T.closest, T.best);
+        if (T.best != before) T.slot = slot;
+    }
+}
+
 __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& sv, const D3& org, const D3& dir) {
     T.a = length_sq(dir);  // hoisted: same bits as per sphere
     T.a_inv = rcp_cr(T.a);
@@ -460,18 +473,11 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& sv, const D
     T.near_x = ix < 0.0f ? kPlane : 0;
     T.near_y = 2 * kPlane + (iy < 0.0f ? kPlane : 0);
     T.near_z = 4 * kPlane + (iz < 0.0f ? kPlane : 0);
-    // The spheres kept out of the tree (tray_bvh.cpp) are visited first; a hit
-    // seeds the culling distance of the whole traversal.
-    for (int32_t g = 0; g < sv.n_global; ++g) {
-        const int32_t slot = sv.global_first + g;
-        double h, d;
-        quad(sv.bgeo[slot], org, dir, T.a, h, d);
-        if (d >= 0) {
-            const int32_t before = T.best;
-            candidate_any_order(h, d, T.a, T.a_inv, sv.bidx[slot], T.closest, T.best);
-            if (T.best != before) T.slot = slot;
-        }
-    }
+    // The spheres kept out of the tree (tray_bvh.cpp, at most kBvhGlobals) are
+    // visited first; a hit seeds the culling distance of the whole traversal.
+#pragma unroll
+    for (int32_t g = 0; g < kBvhGlobals; ++g)
+        if (g < sv.n_global) test_slot(T, sv, sv.global_first + g, org, dir);
     T.tlim = f32_up(T.closest);
 }
 
@@ -606,20 +612,17 @@ template <class Stk>
 __device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const Stk& S, const D3& org,
                                               const D3& dir, uint32_t& tested) {
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for the pop
-    // One sphere per leaf: the leaf index is its slot (no leaf-table round trip).
-    const int32_t info = sv.single ? (int32_t)(((T.cur & (kBvhLeafBit - 1u)) << 3) | 1u)
-                                   : sv.leaves[T.cur & (kBvhLeafBit - 1u)];
-    const int32_t first = info >> 3, end = first + (info & 7);
-    tested = 0;
-    for (int32_t slot = first; slot < end; ++slot) {
-        double h, d;
-        quad(sv.bgeo[slot], org, dir, T.a, h, d);
-        if (d >= 0) {
-            const int32_t before = T.best;
-            candidate_any_order(h, d, T.a, T.a_inv, sv.bidx[slot], T.closest, T.best);
-            if (T.best != before) T.slot = slot;
+    if (sv.single) {  // one sphere per leaf: the leaf index is its slot (no leaf table, no loop)
+        test_slot(T, sv, (int32_t)(T.cur & (kBvhLeafBit - 1u)), org, dir);
+        tested = 1;
+    } else {
+        const int32_t info = sv.leaves[T.cur & (kBvhLeafBit - 1u)];
+        const int32_t first = info >> 3, end = first + (info & 7);
+        tested = 0;
+        for (int32_t slot = first; slot < end; ++slot) {
+            test_slot(T, sv, slot, org, dir);
+            ++tested;
         }
-        ++tested;
     }
     T.tlim = f32_up(T.closest);
     T.cur = stack_pop(T, S, below);
