@@ -401,10 +401,9 @@ constexpr size_t kStackSlotBytes = (size_t)kBvhBlock * sizeof(uint32_t);
 // are in LDS, slot i of the lane at base[i * kBvhBlock] (consecutive lanes,
 // consecutive banks); a scene whose bound is deeper keeps the rest in a global
 // overflow area (spill set: one wave-uniform branch per access otherwise).
-template <bool kSpill, int kLanes = kBvhBlock>
+template <bool kSpill>
 struct Stack {
     static constexpr bool spill = kSpill;
-    static constexpr int lanes = kLanes;  // stride between a lane's slots (lanes sharing the stack area)
     __attribute__((address_space(3))) uint32_t* base;  // this lane's slot 0
     uint32_t* ovf;     // this lane's slot `lds` in the overflow area (stride: grid lanes)
     uint32_t stride;
@@ -415,7 +414,7 @@ template <class Stk>
 __device__ __forceinline__ uint32_t stack_load(const Stk& S, int32_t i) {
     if constexpr (Stk::spill)
         if (i >= S.lds) return S.ovf[(size_t)(i - S.lds) * S.stride];
-    return S.base[i * Stk::lanes];
+    return S.base[i * kBvhBlock];
 }
 
 template <class Stk>
@@ -426,7 +425,7 @@ __device__ __forceinline__ void stack_store(const Stk& S, int32_t i, uint32_t v)
             return;
         }
     }
-    S.base[i * Stk::lanes] = v;
+    S.base[i * kBvhBlock] = v;
 }
 
 // Sort key of a hit child: the upper 16 bits of its entry distance (tn >= 0, so
@@ -944,321 +943,6 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 // wave's slowest ray: it shades and starts its next segment while others still
 // traverse.
 
-// ---------------------------------------------------------------------------
-// Wave-specialised BVH schedule (TRAY_SPEC). The workgroup's waves
-// take one of two roles:
-//   * path waves (kSpecPathWaves) own the paths: camera rays (refill), the
-//     shading of each segment's hit and the out-of-tree spheres' tests; each
-//     new segment is posted as a trace request;
-//   * traversal waves (kSpecTravWaves) take requests into whichever lanes are
-//     free, run the node and leaf phases (the FP32 box tests and FP64 sphere
-//     tests of Scene.Hit) and post the closest hit back.
-// So a node step runs with the lanes of every path that is traversing, not with
-// the lanes of one wave's paths that happen to be, and a path waiting for a
-// batch waits in a wave that issues nothing. Requests and results live in fixed
-// per-path LDS slots (SoA by path index), handed over with one 64-bit ready /
-// done mask per path wave (LDS atomic or / and). The arithmetic of every path
-// is the same function calls in the same order as the one-role kernel, so
-// frames are bit-identical.
-#ifndef TRAY_SPEC_TRAV_WAVES
-#define TRAY_SPEC_TRAV_WAVES 8
-#endif
-#ifndef TRAY_SPEC_SHADE_BATCH
-#define TRAY_SPEC_SHADE_BATCH 40
-#endif
-#ifndef TRAY_SPEC_REFILL_BATCH
-#define TRAY_SPEC_REFILL_BATCH 24
-#endif
-#ifndef TRAY_SPEC_CLAIM_BATCH
-#define TRAY_SPEC_CLAIM_BATCH 16
-#endif
-constexpr int kSpecTravWaves = TRAY_SPEC_TRAV_WAVES;
-constexpr int kSpecPathWaves = kBvhBlock / 64 - kSpecTravWaves;
-constexpr int kSpecPaths = kSpecPathWaves * 64;
-constexpr int kSpecTravLanes = kSpecTravWaves * 64;
-static_assert(kSpecTravWaves >= 1 && kSpecPathWaves >= 1, "TRAY_SPEC_TRAV_WAVES");
-
-// Per-path request / result slots. A request is the segment's ray, its
-// Scene.Hit setup (a, 1/a) and the best hit among the out-of-tree spheres; the
-// traversal overwrites closest/hit with the final answer.
-struct SpecLds {
-    double ox[kSpecPaths], oy[kSpecPaths], oz[kSpecPaths];
-    double dx[kSpecPaths], dy[kSpecPaths], dz[kSpecPaths];
-    double a[kSpecPaths], a_inv[kSpecPaths], closest[kSpecPaths];
-    uint64_t hit[kSpecPaths];          // best (list index) | slot << 32
-    uint64_t ready[kSpecPathWaves];    // requests posted, not yet taken by a traversal lane
-    uint64_t done[kSpecPathWaves];     // results posted, not yet taken by the path wave
-    uint32_t path_waves_done;
-};
-typedef __attribute__((address_space(3))) SpecLds* SpecPtr;
-typedef __attribute__((address_space(3))) uint64_t LdsU64;
-constexpr size_t kSpecLdsBytes = (sizeof(SpecLds) + 255) / 256 * 256;
-
-__device__ __forceinline__ uint64_t lds_uniform_u64(const LdsU64* a) {
-    const uint64_t v = *(const volatile LdsU64*)a;
-    // (the builtin returns int: widen through uint32_t, or the low word sign-extends)
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-    return ((uint64_t)hi << 32) | lo;
-}
-// Data stores to LDS before the mask update that publishes them (one wave's
-// LDS operations complete in order; the fence also keeps the compiler's order).
-__device__ __forceinline__ void lds_publish_fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
-
-// Position of the n-th (0-based) set bit of m (n < popcount(m)).
-__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t n) {
-    uint32_t pos = 0;
-#pragma unroll
-    for (uint32_t w = 32; w >= 1; w >>= 1) {
-        const uint64_t lo = m & ((1ull << w) - 1ull);
-        const uint32_t c = (uint32_t)__popcll(lo);
-        const bool up = n >= c;
-        n -= up ? c : 0u;
-        m = up ? m >> w : lo;
-        pos += up ? w : 0u;
-    }
-    return pos;
-}
-// The lowest n set bits of m.
-__device__ __forceinline__ uint64_t lowest_set_bits(uint64_t m, uint32_t n) {
-    if ((uint32_t)__popcll(m) <= n) return m;
-    const uint32_t b = nth_set_bit(m, n);  // first bit not taken
-    return m & ((1ull << b) - 1ull);
-}
-
-__device__ __forceinline__ uint64_t pack_hit(int32_t best, int32_t slot) {
-    return ((uint64_t)(uint32_t)slot << 32) | (uint32_t)best;
-}
-
-// Post the request of path `pid` (the lane's current segment).
-__device__ __forceinline__ void spec_post(SpecPtr A, uint32_t pid, const Lane& L, const Trav& H) {
-    A->ox[pid] = L.org.x, A->oy[pid] = L.org.y, A->oz[pid] = L.org.z;
-    A->dx[pid] = L.dir.x, A->dy[pid] = L.dir.y, A->dz[pid] = L.dir.z;
-    A->a[pid] = H.a, A->a_inv[pid] = H.a_inv, A->closest[pid] = H.closest;
-    A->hit[pid] = pack_hit(H.best, H.slot);
-}
-
-template <bool kStats, bool kProg>
-__device__ __forceinline__ void spec_path_wave(const KernelParams& p, UniPtr uni, const SceneView& sv, SpecPtr A,
-                                               uint32_t pw, uint32_t lane, Stats& st) {
-    const uint32_t pid = pw * 64u + lane;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    Lane L;
-    L.busy = false;
-    bool tracing = false;
-    uint32_t pool_next = 0, pool_end = 0;
-    bool exhausted = false;
-    int32_t prog_cur = 0;
-    uint32_t prog_cnt = 0;
-    LdsU64* ready = &A->ready[pw];
-    LdsU64* done = &A->done[pw];
-#ifdef TRAY_SPEC_WATCHDOG
-    uint32_t spins = 0;
-#endif
-    while (true) {
-        bool worked = false;
-        // Shade the segments whose hits came back, once enough did (or all).
-        const uint64_t back = lds_uniform_u64(done);
-        const uint32_t n_out = (uint32_t)__popcll(__ballot(tracing));
-        if (back != 0ull && ((uint32_t)__popcll(back) >= TRAY_SPEC_SHADE_BATCH || (uint32_t)__popcll(back) == n_out)) {
-            if (lane == 0) __hip_atomic_fetch_and(done, ~back, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            asm volatile("" ::: "memory");  // the results are read after the mask (LDS executes a wave's operations in order)
-            worked = true;
-            bool ended = false, posted = false;
-            if ((back >> lane) & 1ull) {
-                tracing = false;
-                const double closest = A->closest[pid];
-                const uint64_t hit = A->hit[pid];
-                const int32_t best = (int32_t)(uint32_t)hit, slot = (int32_t)(hit >> 32);
-                const double a = A->a[pid];
-                if (shade_step<kStats>(p, uni, L, best, closest, a, [&] { return sv.bgeo[slot]; },
-                                       [&] { return sv.bmat[slot]; }, st)) {
-                    ++L.segments;
-                    Trav H;
-                    trav_globals(H, sv, L.org, L.dir);
-                    if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
-                    spec_post(A, pid, L, H);
-                    posted = tracing = true;
-                } else {
-                    ended = true;
-                }
-            }
-            if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
-            const uint64_t m = __ballot(posted);
-            if (m != 0ull) {
-                lds_publish_fence();
-                if (lane == 0) __hip_atomic_fetch_or(ready, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-        // Refill idle lanes with new samples (a batch, or whatever is idle when
-        // nothing of this wave is in flight).
-        uint64_t idle = __ballot(!L.busy);
-        if (!exhausted && idle != 0ull &&
-            ((uint32_t)__popcll(idle) >= TRAY_SPEC_REFILL_BATCH || __ballot(tracing) == 0ull)) {
-            uint32_t fresh_item = ~0u;
-            while (idle != 0ull && !exhausted) {
-                if (pool_next == pool_end) {
-                    const uint32_t c = take_chunk(p, uni, lane);
-                    if (c == kPoolDone) {
-                        exhausted = true;
-                        break;
-                    }
-                    pool_next = c * 64u;
-                    pool_end = pool_next + 64u;
-                }
-                const uint32_t n_idle = (uint32_t)__popcll(idle);
-                const uint32_t take = min(n_idle, pool_end - pool_next);
-                if ((idle >> lane) & 1ull) {
-                    const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
-                    if (rank < take) fresh_item = pool_next + rank;
-                }
-                pool_next += take;
-                idle = __ballot(!L.busy && fresh_item == ~0u);
-            }
-            bool posted = false;
-            if (fresh_item != ~0u) {
-                int32_t x, j;
-                uint32_t smp, pass;
-                if (fresh_item < p.items && decode_item(p, fresh_item, x, j, smp, pass)) {
-                    start_sample(p, uni, L, fresh_item, x, j, (p.pass0 + pass) * (uint32_t)p.spp + smp);
-                    ++L.segments;
-                    Trav H;
-                    trav_globals(H, sv, L.org, L.dir);
-                    if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
-                    spec_post(A, pid, L, H);
-                    posted = tracing = true;
-                }
-            }
-            const uint64_t m = __ballot(posted);
-            if (m != 0ull) {
-                lds_publish_fence();
-                if (lane == 0) __hip_atomic_fetch_or(ready, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            worked = true;
-        }
-        if (__ballot(L.busy) == 0ull && exhausted) break;
-        if (!worked) __builtin_amdgcn_s_sleep(1);
-#ifdef TRAY_SPEC_WATCHDOG
-        if (++spins > (1u << 22)) {
-            const uint64_t bz = __ballot(L.busy), tr = __ballot(tracing);
-            if (lane == 0 && blockIdx.x < 2)
-                printf("WD path b%u pw%u busy %llx tracing %llx done %llx ready %llx exh %d pool %u/%u left %u\n", blockIdx.x, pw,
-                       (unsigned long long)bz, (unsigned long long)tr, (unsigned long long)lds_uniform_u64(done),
-                       (unsigned long long)lds_uniform_u64(ready), (int)exhausted, pool_next, pool_end, A->path_waves_done);
-            break;
-        }
-#endif
-    }
-    if constexpr (kProg) flush_progress(p, prog_cur, prog_cnt, lane);
-    if (lane == 0) __hip_atomic_fetch_add(&A->path_waves_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <bool kStats, class Stk>
-__device__ __forceinline__ void spec_trav_wave(const KernelParams& p, const SceneView& sv, const Stk& S, SpecPtr A,
-                                               uint32_t tw, uint32_t lane, Stats& st) {
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    Trav T;
-    T.cur = kBvhNone;
-    D3 org = d3(0, 0, 0), dir = d3(0, 0, 0);
-    uint32_t pid = 0;
-    bool busy = false;
-    uint32_t start = tw % (uint32_t)kSpecPathWaves;  // first path wave to take requests from (rotates)
-#ifdef TRAY_SPEC_WATCHDOG
-    uint32_t spins = 0;
-#endif
-    while (true) {
-        bool worked = false;
-        // Take posted requests into the free lanes.
-        const uint64_t idle = __ballot(!busy);
-        if (idle != 0ull && ((uint32_t)__popcll(idle) >= TRAY_SPEC_CLAIM_BATCH || idle == ~0ull)) {
-            uint32_t need = (uint32_t)__popcll(idle), got_n = 0, mine = ~0u;
-            const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
-            for (int k = 0; k < kSpecPathWaves && need != 0u; ++k) {
-                uint32_t w = start + (uint32_t)k;
-                if (w >= (uint32_t)kSpecPathWaves) w -= (uint32_t)kSpecPathWaves;
-                const uint64_t r = lds_uniform_u64(&A->ready[w]);
-                if (r == 0ull) continue;
-                const uint64_t want = lowest_set_bits(r, need);
-                uint64_t old = 0;
-                if (lane == 0) old = __hip_atomic_fetch_and(&A->ready[w], ~want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const uint32_t old_hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(old >> 32), 0);
-                const uint32_t old_lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)old, 0);
-                const uint64_t got = (((uint64_t)old_hi << 32) | old_lo) & want;
-                const uint32_t n = (uint32_t)__popcll(got);
-                if (!busy && rank >= got_n && rank < got_n + n) mine = w * 64u + nth_set_bit(got, rank - got_n);
-                got_n += n;
-                need -= n;
-            }
-            start = start + 1u == (uint32_t)kSpecPathWaves ? 0u : start + 1u;
-            if (mine != ~0u) {
-                pid = mine;
-                org = d3(A->ox[pid], A->oy[pid], A->oz[pid]);
-                dir = d3(A->dx[pid], A->dy[pid], A->dz[pid]);
-                T.a = A->a[pid];
-                T.a_inv = A->a_inv[pid];
-                T.closest = A->closest[pid];
-                const uint64_t hit = A->hit[pid];
-                T.best = (int32_t)(uint32_t)hit;
-                T.slot = (int32_t)(hit >> 32);
-                trav_begin32(T, sv, org, dir);
-                busy = true;
-            }
-            worked = got_n != 0u;
-        }
-        // Node steps for the traversing lanes.
-#pragma unroll 1
-        for (int s = 0; s < TRAY_NODE_STEPS; ++s) {
-            if (__ballot(is_trav(T.cur)) == 0ull) break;
-            worked = true;
-            if (is_trav(T.cur)) {
-                uint32_t tested;
-                trav_node(T, sv, S, tested);
-                if constexpr (kStats) st.boxes += tested;
-            }
-        }
-        // Leaf phase: FP64 sphere tests, batched.
-        const uint64_t m_leaf = __ballot(is_leaf(T.cur));
-        if (m_leaf != 0ull && ((uint32_t)__popcll(m_leaf) >= TRAY_LEAF_BATCH || __ballot(is_trav(T.cur)) == 0ull)) {
-            worked = true;
-            if (is_leaf(T.cur)) {
-                uint32_t tested;
-                trav_leaf(T, sv, S, org, dir, tested);
-                if constexpr (kStats) st.spheres += tested;
-            }
-        }
-        // Hand finished hits back to their path waves.
-        const bool fin = busy && T.cur == kBvhNone;
-        if (__ballot(fin) != 0ull) {
-            worked = true;
-            if (fin) {
-                A->closest[pid] = T.closest;
-                A->hit[pid] = pack_hit(T.best, T.slot);
-                lds_publish_fence();
-                __hip_atomic_fetch_or(&A->done[pid >> 6], 1ull << (pid & 63u), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                busy = false;
-            }
-        }
-        if (__ballot(busy) == 0ull) {
-            // Every path wave has left: nothing is in flight and nothing will be posted.
-            const uint32_t left = __builtin_amdgcn_readfirstlane(*(const volatile __attribute__((address_space(3))) uint32_t*)&A->path_waves_done);
-            if (left == (uint32_t)kSpecPathWaves) break;
-        }
-        if (!worked) __builtin_amdgcn_s_sleep(1);
-#ifdef TRAY_SPEC_WATCHDOG
-        if (++spins > (1u << 22)) {
-            const uint64_t bz = __ballot(busy), tv = __ballot(is_trav(T.cur)), lf = __ballot(is_leaf(T.cur));
-            if (lane == 0 && blockIdx.x < 2)
-                printf("WD trav b%u tw%u busy %llx trav %llx leaf %llx ready0 %llx done0 %llx left %u\n", blockIdx.x, tw,
-                       (unsigned long long)bz, (unsigned long long)tv, (unsigned long long)lf,
-                       (unsigned long long)lds_uniform_u64(&A->ready[0]), (unsigned long long)lds_uniform_u64(&A->done[0]),
-                       A->path_waves_done);
-            break;
-        }
-#endif
-    }
-}
-
 // LDS bytes of `slots` stack slots of a BVH workgroup (32-bit entries).
 __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (size_t)slots * kStackSlotBytes; }
 
@@ -1266,10 +950,8 @@ __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (si
 // LDS with sphere geometry in global memory (scenes too big for 1; BVH only).
 // kProg: the live-progress instance (tray_render_progress only), so the other
 // instances carry no progress code or registers.
-// kSpec: the wave-specialised schedule (BVH only, whole stack in LDS).
-template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg, bool kSpec = false>
+template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg>
 __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
-    static_assert(!kSpec || (kBVH && !kSpill), "the specialised schedule needs the BVH and an on-chip stack");
     extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
     __attribute__((address_space(3))) Uniforms* uni_lds =
         (__attribute__((address_space(3))) Uniforms*)reinterpret_cast<Uniforms*>(smem_all);
@@ -1302,21 +984,11 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         // [stacks: stack_cap x blockDim x 4 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]
         // [bidx: n_slots x 4 B][leaves: n_leaves x 4 B]; shading records (bmat) stay
         // in global memory (L1/L2-resident, read once per hit).
-        // Specialised schedule: [SpecLds][stacks: stack_cap x traversal lanes x 4 B][scene].
-        const size_t spec_bytes = kSpec ? kSpecLdsBytes : 0;
-        const size_t stack_bytes =
-            kSpec ? ((size_t)p.stack_lds * kSpecTravLanes * sizeof(uint32_t) + 31) / 32 * 32 : bvh_stack_bytes(p.stack_lds);
-        S.base = (__attribute__((address_space(3))) uint32_t*)reinterpret_cast<uint32_t*>(smem + spec_bytes / sizeof(double4)) +
-                 threadIdx.x;
+        S.base = (__attribute__((address_space(3))) uint32_t*)reinterpret_cast<uint32_t*>(smem) + threadIdx.x;
         S.lds = p.stack_lds;
         S.stride = gridDim.x * blockDim.x;
         if constexpr (kSpill) S.ovf = p.stack_ovf + blockIdx.x * blockDim.x + threadIdx.x;
-        double4* scene = smem + (spec_bytes + stack_bytes) / sizeof(double4);
-        if constexpr (kSpec) {
-            SpecLds* A = reinterpret_cast<SpecLds*>(smem);
-            if (threadIdx.x < (unsigned)kSpecPathWaves) A->ready[threadIdx.x] = 0ull, A->done[threadIdx.x] = 0ull;
-            if (threadIdx.x == 0) A->path_waves_done = 0u;
-        }
+        double4* scene = smem + bvh_stack_bytes(p.stack_lds) / sizeof(double4);
         if constexpr (kLDS == 1) {
             double4* lds_nodes = scene;
             double4* lds_geo = scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4));
@@ -1353,23 +1025,6 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    if constexpr (kSpec) {
-        const SpecPtr A = (SpecPtr)reinterpret_cast<SpecLds*>(smem);
-        const uint32_t wi = threadIdx.x / 64u;
-        Stats st;
-        if (wi < (uint32_t)kSpecTravWaves) {  // waves wi and wi + 4k share a SIMD: the roles interleave
-            Stack<false, kSpecTravLanes> TS{S.base, nullptr, 0, p.stack_lds};  // S.base is this lane's slot 0 (threadIdx.x < traversal lanes)
-            spec_trav_wave<kStats>(p, sv, TS, A, wi, lane, st);
-        } else {
-            spec_path_wave<kStats, kProg>(p, uni, sv, A, wi - (uint32_t)kSpecTravWaves, lane, st);
-        }
-        if constexpr (kStats) {
-            atomicAdd(p.stats + 0, (unsigned long long)st.segments);
-            atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
-            atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
-        }
-        return;
-    }
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     Lane L;
     L.busy = false;
@@ -1696,25 +1351,6 @@ static KernelFn pick_kernel2(int lds_mode, bool stats, bool progress) {
     return pick_kernel3<kBVH, kSpill, false, false>(lds_mode);
 }
 
-template <bool kStats, bool kProg>
-static KernelFn pick_spec2(int lds_mode) {
-    if (lds_mode == 1) return render_kernel<1, true, kStats, false, kProg, true>;
-    return render_kernel<2, true, kStats, false, kProg, true>;
-}
-static KernelFn pick_spec(int lds_mode, bool stats, bool progress) {
-    if (stats) return pick_spec2<true, false>(lds_mode);
-    if (progress) return pick_spec2<false, true>(lds_mode);
-    return pick_spec2<false, false>(lds_mode);
-}
-
-static bool spec_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("TRAY_SPEC");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
 static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, bool spill) {
     if (!bvh) return pick_kernel2<false, false>(lds_mode, stats, progress);
     return spill ? pick_kernel2<true, true>(lds_mode, stats, progress)
@@ -1817,14 +1453,6 @@ bool band_fits(int32_t width, uint64_t spp) {
     return (uint64_t)((width + 7) / 8) * 64u * spp <= 0x7FFFFFFFull;
 }
 
-// LDS of the specialised schedule for a scene layout (1: whole scene, 2: nodes
-// and leaf table), or 0 when it does not fit (whole stack on chip, no overflow).
-static size_t spec_lds_bytes(const KernelParams& p, int mode) {
-    const size_t scene = mode == 1 ? scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves) : nodes_lds_bytes(p.n_nodes, p.n_leaves);
-    const size_t b = kUniformsBytes + kSpecLdsBytes + ((size_t)p.stack_cap * kSpecTravLanes * sizeof(uint32_t) + 31) / 32 * 32 + scene;
-    return b <= kMaxLDSBytes ? b : 0;
-}
-
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (p.rows <= 0) return hipSuccess;
     if (p.passes < 1) p.passes = 1;
@@ -1838,7 +1466,6 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     int lds_mode;
-    int spec_mode = 0;  // the specialised schedule's scene layout (0: one-role schedule)
     size_t lds;
     if (use_bvh) {
         // Whole scene in LDS when it fits next to kStackLdsMin stack slots, else
@@ -1860,15 +1487,6 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
             p.stack_lds = std::min(p.stack_lds, std::max<int32_t>(kStackLdsMin, atoi(cap)));
         if (p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
         lds = kUniformsBytes + bvh_stack_bytes(p.stack_lds) + scene;
-        if (spec_enabled() && lds_mode != 0) {
-            int mode = spec_lds_bytes(p, 1) ? 1 : spec_lds_bytes(p, 2) ? 2 : 0;
-            if (mode == 2 && lds_mode == 1 && spec_lds_bytes(p, 1) == 0) mode = 2;
-            if (mode != 0) {
-                spec_mode = mode;
-                lds = spec_lds_bytes(p, mode);
-                p.stack_lds = p.stack_cap;
-            }
-        }
     } else {
         const size_t geo = (size_t)p.n_pad * sizeof(double4);
         lds_mode = geo + kUniformsBytes <= kMaxLDSBytes ? 1 : 0;
@@ -1876,8 +1494,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     }
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
-    const KernelFn fn = spec_mode ? pick_spec(spec_mode, stats, p.progress != nullptr)
-                                  : pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr, use_bvh && p.stack_cap > p.stack_lds);
+    const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr, use_bvh && p.stack_cap > p.stack_lds);
     const KernelFn resolve = pick_resolve(p.out_format, p.spp);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {
