@@ -116,6 +116,13 @@ static int device_state(int32_t device, DeviceState** out) {
 // A scene resident on one device. Renders of one scene handle share its work
 // queue counter, so they must be ordered on one stream (the queue is zero when
 // a launch starts: zeroed at allocation, then by each band's resolve pass).
+// What a primary-ray candidate list depends on (compared byte for byte).
+struct CandKey {
+    tray_camera cam;
+    double ray_radius;
+    int32_t width, height, y_start, rows, tile_rows, tile_count, tile_index, multi_sample;
+};
+
 struct tray_scene_s {
     int32_t device;
     int32_t n;
@@ -139,6 +146,12 @@ struct tray_scene_s {
     double* samples;
     size_t samples_bytes;
     double* srgb;  // the RGBA8 encoder table (tray::srgb_thresholds), 256 doubles
+    // Primary-ray candidates of the last camera and row set rendered (BVH scenes;
+    // launch_cand_build), rebuilt on the render stream when either changes.
+    uint4* cand;
+    size_t cand_bytes;
+    bool cand_valid;
+    CandKey cand_key;
 };
 
 using namespace tray;
@@ -296,6 +309,9 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->samples = nullptr;
     sc->samples_bytes = 0;
     sc->srgb = nullptr;
+    sc->cand = nullptr;
+    sc->cand_bytes = 0;
+    sc->cand_valid = false;
     std::vector<MatRec> bmat(bvh.idx.size());
     for (size_t i = 0; i < bvh.idx.size(); ++i) {
         const int32_t k = bvh.idx[i];
@@ -383,8 +399,18 @@ int tray_scene_release(tray_scene_t sc) {
     if (sc->bmat) (void)hipFree(sc->bmat);
     if (sc->samples) (void)hipFree(sc->samples);
     if (sc->srgb) (void)hipFree(sc->srgb);
+    if (sc->cand) (void)hipFree(sc->cand);
     delete sc;
     return TRAY_OK;
+}
+
+// Primary-ray candidate lists (on unless TRAY_PRIMARY_CANDIDATES=0, an A/B and
+// test switch), for scenes whose tree has at most kCandMaxSpheres spheres (the
+// list build tests every tree sphere against every pixel's beam).
+constexpr int32_t kCandMaxSpheres = 8192;
+static bool cand_enabled() {
+    const char* e = getenv("TRAY_PRIMARY_CANDIDATES");
+    return !(e && *e && atoi(e) == 0);
 }
 
 static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
@@ -468,6 +494,34 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         sc->samples_bytes = need;
     }
     k.samples = sc->samples;
+    if (use_bvh && cand_enabled() && sc->n_slots - sc->n_global <= kCandMaxSpheres) {
+        CandKey key;
+        memset(&key, 0, sizeof(key));
+        key.cam = *cam;
+        key.ray_radius = p->ray_radius;
+        key.width = p->width, key.height = p->height, key.y_start = p->y_start, key.rows = k.rows;
+        key.tile_rows = k.tile_rows, key.tile_count = k.tile_count, key.tile_index = k.tile_index;
+        key.multi_sample = p->rays_per_pixel > 1;
+        if (!sc->cand_valid || memcmp(&key, &sc->cand_key, sizeof(key)) != 0) {
+            const size_t bytes = (size_t)k.rows * (size_t)p->width * sizeof(uint4);
+            if (bytes > sc->cand_bytes) {
+                if (sc->cand) {
+                    TRAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+                    TRAY_HIP(hipFree(sc->cand));
+                    sc->cand = nullptr;
+                    sc->cand_bytes = 0;
+                }
+                sc->cand_valid = false;
+                TRAY_HIP(hipMalloc(&sc->cand, bytes));
+                sc->cand_bytes = bytes;
+            }
+            sc->cand_valid = false;
+            TRAY_HIP(launch_cand_build(k, sc->cand, static_cast<hipStream_t>(stream)));
+            sc->cand_key = key;
+            sc->cand_valid = true;
+        }
+        k.cand = sc->cand;
+    }
     TRAY_HIP(launch_render(k, use_bvh, static_cast<hipStream_t>(stream)));
     return TRAY_OK;
 }

@@ -1085,11 +1085,33 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #ifdef TRAY_PROBE_REFILL
                 TRAY_PROBE_F32(TRAY_PROBE_REFILL)
 #endif
+                // The pixel's primary-ray candidates, loaded before the camera ray is built.
+                uint4 cand = make_uint4(0u, 0u, 0u, kCandOverflow << 16);
+                if constexpr (kBVH)
+                    if (p.cand) cand = p.cand[(size_t)j * (size_t)p.width + (size_t)x];
                 start_sample(p, uni, L, fresh_item, x, j, (p.pass0 + pass) * (uint32_t)p.spp + smp);
                 if constexpr (kBVH) {
                     ++L.segments;
-                    trav_begin(T, sv, L.org, L.dir);
+                    T.tlim = __builtin_inff();
+                    trav_globals(T, sv, L.org, L.dir);
                     if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
+                    const uint32_t n_cand = cand.w >> 16;
+                    if (n_cand <= kCandSlots) {
+                        // Scene.Hit of a camera ray: the out-of-tree spheres and the pixel's
+                        // candidates under the any-order rule (every other tree sphere is out
+                        // of the ray's reach), no traversal.
+                        uint64_t lo = ((uint64_t)cand.y << 32) | cand.x, hi = ((uint64_t)cand.w << 32) | cand.z;
+#pragma unroll 1
+                        for (uint32_t k = 0; k < n_cand; ++k) {
+                            test_slot(T, sv, (int32_t)(lo & 0xFFFFu), L.org, L.dir);
+                            lo = (lo >> 16) | (hi << 48);
+                            hi >>= 16;
+                        }
+                        if constexpr (kStats) st.spheres += n_cand;
+                        T.cur = kBvhNone;  // traversal done: the lane waits for the shade phase
+                    } else {
+                        trav_begin32(T, sv, L.org, L.dir);
+                    }
                 }
             }
         }
@@ -1312,6 +1334,76 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
         for (; s < p.spp; ++s) sum = add(sum, d3(smp[3 * s], smp[3 * s + 1], smp[3 * s + 2]));
     }
     if (valid) write_mean<kFmt>(p, srgb, sum, x, j, pass);
+}
+
+// Primary-ray candidates (launch_cand_build). A camera ray of pixel (x, y)
+// (get_ray) runs from a lens point o = pos + du dx + dv dy, |(dx, dy)| <= 1, through
+// F = pos + (S - pos) ft (aperture > 0; F = S otherwise), S = p00 + px (x + ox) +
+// py (y + oy), |(ox, oy)| <= ray_radius (when r > 1). With A0 = pos, B0 = the
+// disc centre's F and D = B0 - A0, the ray's point at parameter t is
+// (1 - t) o + t F, within w(t) = |1 - t| rA + t rB of the axis point A0 + t D
+// (rA, rB: the two disc radii). A sphere (C, R) the ray enters at t >= 0
+// therefore satisfies |A0 + t D - C| <= R + w(t). With tc = the axis parameter
+// closest to C (clamped to t >= 0), d_perp = C's distance from the axis line and
+// L = rA + rB (w's slope bound): |t - tc| |D| <= R + w(tc) + L |t - tc| gives
+// |t - tc| <= (R + w(tc)) / (|D| - L), hence the necessary condition
+// d_perp <= R + w(tc) + L (R + w(tc)) / (|D| - L). The margin covers the FP64
+// rounding of both this bound and the kernel's ray (orders of magnitude
+// above it). Spheres outside the tree (kBvhGlobals) are tested for every ray
+// anyway and are not listed.
+__global__ __launch_bounds__(256) void cand_build_kernel(KernelParams p, uint4* out) {
+    const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= (size_t)p.rows * (size_t)p.width) return;
+    const int32_t j = (int32_t)(i / (size_t)p.width), x = (int32_t)(i % (size_t)p.width);
+    const double y = (double)row_of(p, j);
+    const D3 pos = d3(p.cam.position[0], p.cam.position[1], p.cam.position[2]);
+    const D3 p00 = d3(p.cam.pixel00[0], p.cam.pixel00[1], p.cam.pixel00[2]);
+    const D3 pxv = d3(p.cam.pixel_x[0], p.cam.pixel_x[1], p.cam.pixel_x[2]);
+    const D3 pyv = d3(p.cam.pixel_y[0], p.cam.pixel_y[1], p.cam.pixel_y[2]);
+    const D3 du = d3(p.cam.defocus_u[0], p.cam.defocus_u[1], p.cam.defocus_u[2]);
+    const D3 dv = d3(p.cam.defocus_v[0], p.cam.defocus_v[1], p.cam.defocus_v[2]);
+    const bool lens = p.cam.aperture > 0;
+    const D3 s0 = add(add(p00, smul(pxv, (double)x)), smul(pyv, y));
+    const D3 b0 = lens ? add(pos, smul(sub(s0, pos), p.focus_time)) : s0;
+    const double aa = p.spp > 1 ? p.ray_radius * __builtin_sqrt(length_sq(pxv) + length_sq(pyv)) : 0.0;
+    const double ra = lens ? __builtin_sqrt(length_sq(du) + length_sq(dv)) : 0.0;
+    const double rb = lens ? aa * __builtin_fabs(p.focus_time) : aa;
+    const D3 D = sub(b0, pos);
+    const double dn2 = length_sq(D), dn = __builtin_sqrt(dn2), L = ra + rb;
+    uint32_t slots[kCandSlots];
+    uint32_t n = 0;
+    bool ok = dn > 2.0 * L && dn2 > 0;
+    const double scale = 1.0 + __builtin_fmax(__builtin_fmax(__builtin_fabs(pos.x), __builtin_fabs(pos.y)), __builtin_fabs(pos.z));
+    const int32_t tree = p.n_slots - p.n_global;  // slots of the tree's spheres
+    for (int32_t s = 0; s < tree && ok; ++s) {
+        const double4 g = p.bgeo[s];
+        const double R = __builtin_fabs(p.bmat[s].radius);
+        const D3 rel = sub(d3(g.x, g.y, g.z), pos);
+        const double tc = dot(rel, D) / dn2;
+        const double tcl = __builtin_fmax(tc, 0.0);
+        const double dperp = __builtin_sqrt(length_sq(sub(rel, smul(D, tc))));
+        const double margin = 1e-6 * (scale + __builtin_fabs(g.x) + __builtin_fabs(g.y) + __builtin_fabs(g.z) + R);
+        const double reach = R + __builtin_fabs(1.0 - tcl) * ra + tcl * rb + margin;
+        if (dperp <= reach + L * reach / (dn - L) + margin || !(dperp == dperp)) {
+            if (n == kCandSlots) ok = false;
+            else slots[n++] = (uint32_t)s;
+        }
+    }
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (ok) {
+#pragma unroll
+        for (uint32_t k = 0; k < kCandSlots; ++k)
+            if (k < n) w[k >> 1] |= slots[k] << (16u * (k & 1u));
+    }
+    w[3] = (w[3] & 0xFFFFu) | ((ok ? n : kCandOverflow) << 16);
+    out[i] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+hipError_t launch_cand_build(const KernelParams& p, uint4* out, hipStream_t stream) {
+    const size_t n = (size_t)p.rows * (size_t)p.width;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(cand_build_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, p, out);
+    return hipGetLastError();
 }
 
 // ColorF.ToSRGBA over a device buffer of linear colours (tray_linear_to_srgba_async).

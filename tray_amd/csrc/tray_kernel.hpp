@@ -103,9 +103,21 @@ struct KernelParams {
     uint32_t* segments;
     const double* srgb;  // TRAY_OUT_RGBA8: the 256-entry encoder table (tray::srgb_thresholds)
     uint32_t* progress;  // nullable, HOST-mapped: samples finished per 8-row tile row of the compact rows
+    const uint4* cand;   // nullable (BVH only): primary-ray candidate record per compact pixel (launch_cand_build)
 };
 
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
+
+// Primary-ray candidates: for every compact pixel of p's rows, the
+// tree spheres (leaf slots) that any camera ray of the pixel can reach, by a
+// conservative bound on the beam from the lens disc through the pixel's
+// anti-aliasing disc; a record holds up to kCandSlots slots, or
+// kCandOverflow (that pixel's camera rays traverse the BVH). `out` holds
+// rows x width records. Needs p's camera, image, row, BVH geometry and shading
+// record fields.
+constexpr uint32_t kCandSlots = 7;
+constexpr uint32_t kCandOverflow = 0xFFFFu;
+hipError_t launch_cand_build(const KernelParams& p, uint4* out, hipStream_t stream);
 
 // ColorF.ToSRGBA over n device pixels (3 doubles each) into RGBA8 words, with the
 // threshold table `srgb` (device, 256 doubles) that makes it bit-identical to the
