@@ -151,3 +151,28 @@ def test_candidate_cache_follows_camera_and_rows(L, O):
             ref, _ = L.render(spheres, bg_struct(L, DEFAULT_BG), st, p, 0)
         assert np.array_equal(out.cpu().numpy(), ref)
     sc.release()
+
+
+def test_candidates_equal_traversal_random_cameras(L, O):
+    """24 random cameras (position inside and outside the spheres, any target,
+    field of view 5-150 degrees, aperture 0-3, focus 0.5-30, AA radius 0-3) on the
+    adversarial scene and the dense scene: identical frames with and without
+    candidate lists."""
+    rng = np.random.default_rng(2024)
+    scenes = [adversarial(O), O.rich_scene(7, 22)]
+    for k in range(24):
+        sc = scenes[k % 2]
+        span = 8.0 if k % 2 == 0 else 25.0
+        frm = rng.uniform(-span, span, 3)
+        frm[1] = abs(frm[1]) + 0.5
+        at = rng.uniform(-span / 2, span / 2, 3)
+        at[1] = rng.uniform(0, 2)
+        vfov = rng.uniform(5, 150)
+        aperture = 0.0 if k % 4 == 1 else rng.uniform(0, 3)
+        focus = rng.uniform(0.5, 30)
+        setup = np.r_[frm, at, [0, 1, 0], vfov, 1.0, focus, aperture]
+        spp = [1, 2, 4][k % 3]
+        radius = rng.uniform(0, 3)
+        (rgb, seg), (ref, rseg) = both(L, sc, setup, 48, 32, spp, 8, radius, 100 + k)
+        assert np.array_equal(seg, rseg), (k, setup, spp, radius)
+        assert np.array_equal(rgb, ref, equal_nan=True), (k, setup, spp, radius)
