@@ -882,6 +882,13 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #ifndef TRAY_NODE_STEPS
 #define TRAY_NODE_STEPS 3
 #endif
+// Up to TRAY_NODE_STEPS_MAX node steps while at least TRAY_NODE_MORE_LANES lanes still traverse.
+#ifndef TRAY_NODE_STEPS_MAX
+#define TRAY_NODE_STEPS_MAX TRAY_NODE_STEPS
+#endif
+#ifndef TRAY_NODE_MORE_LANES
+#define TRAY_NODE_MORE_LANES 64
+#endif
 #ifndef TRAY_LEAF_BATCH
 #define TRAY_LEAF_BATCH 24
 #endif
@@ -1136,9 +1143,10 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             {
                 PROF_T0();
 #pragma unroll 1
-                for (int s = 0; s < TRAY_NODE_STEPS; ++s) {
+                for (int s = 0; s < TRAY_NODE_STEPS_MAX; ++s) {
                     const uint64_t m = __ballot(is_trav(T.cur));
                     if (m == 0ull) break;
+                    if (s >= TRAY_NODE_STEPS && __popcll(m) < TRAY_NODE_MORE_LANES) break;
                     PROF_CNT(4, 1);
                     PROF_CNT(5, __popcll(m));
                     PROF_CNT(11, __popcll(__ballot(is_leaf(T.cur))));             // waiting for the leaf phase
