@@ -406,8 +406,8 @@ int tray_scene_release(tray_scene_t sc) {
 
 // Primary-ray candidate lists (on unless TRAY_PRIMARY_CANDIDATES=0, an A/B and
 // test switch), for scenes whose tree has at most kCandMaxSpheres spheres (the
-// list build tests every tree sphere against every pixel's beam).
-constexpr int32_t kCandMaxSpheres = 8192;
+// build tests every tree sphere against every 8x8 tile's beam).
+constexpr int32_t kCandMaxSpheres = 16384;
 static bool cand_enabled() {
     const char* e = getenv("TRAY_PRIMARY_CANDIDATES");
     return !(e && *e && atoi(e) == 0);
@@ -503,7 +503,7 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         key.tile_rows = k.tile_rows, key.tile_count = k.tile_count, key.tile_index = k.tile_index;
         key.multi_sample = p->rays_per_pixel > 1;
         if (!sc->cand_valid || memcmp(&key, &sc->cand_key, sizeof(key)) != 0) {
-            const size_t bytes = (size_t)k.rows * (size_t)p->width * sizeof(uint4);
+            const size_t bytes = cand_workspace_bytes(p->width, k.rows);
             if (bytes > sc->cand_bytes) {
                 if (sc->cand) {
                     TRAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));

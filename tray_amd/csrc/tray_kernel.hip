@@ -1359,40 +1359,97 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
 // rounding of both this bound and the kernel's ray (orders of magnitude
 // above it). Spheres outside the tree (kBvhGlobals) are tested for every ray
 // anyway and are not listed.
-__global__ __launch_bounds__(256) void cand_build_kernel(KernelParams p, uint4* out) {
-    const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
-    if (i >= (size_t)p.rows * (size_t)p.width) return;
-    const int32_t j = (int32_t)(i / (size_t)p.width), x = (int32_t)(i % (size_t)p.width);
-    const double y = (double)row_of(p, j);
-    const D3 pos = d3(p.cam.position[0], p.cam.position[1], p.cam.position[2]);
+// The beam test of one sphere against an axis pos + t D (|D|^2 = dn2) with
+// disc radii ra (lens) and rb (far disc): false only when no ray of the beam
+// can reach the sphere (comment above).
+__device__ __forceinline__ bool beam_reaches(const D3& pos, const D3& D, double dn2, double dn, double ra, double rb,
+                                             double scale, double4 g, double R) {
+    const double L = ra + rb;
+    const D3 rel = sub(d3(g.x, g.y, g.z), pos);
+    const double tc = dot(rel, D) / dn2;
+    const double tcl = __builtin_fmax(tc, 0.0);
+    const double dperp = __builtin_sqrt(length_sq(sub(rel, smul(D, tc))));
+    const double margin = 1e-6 * (scale + __builtin_fabs(g.x) + __builtin_fabs(g.y) + __builtin_fabs(g.z) + R);
+    const double reach = R + __builtin_fabs(1.0 - tcl) * ra + tcl * rb + margin;
+    return dperp <= reach + L * reach / (dn - L) + margin || !(dperp == dperp);
+}
+
+// The beam of a rectangle of pixels: columns [xa, xb], image rows [ya, yb] (one
+// pixel: xa = xb, ya = yb). Its far disc is centred on the rectangle's centre
+// and grown by the rectangle's half extent, so it contains every pixel's disc.
+struct Beam {
+    D3 pos, D;
+    double dn2, dn, ra, rb, scale;
+    bool ok;  // false: degenerate (the axis is not longer than twice the disc radii)
+};
+__device__ __forceinline__ Beam pixel_beam(const KernelParams& p, double xa, double xb, double ya, double yb) {
+    Beam b;
+    b.pos = d3(p.cam.position[0], p.cam.position[1], p.cam.position[2]);
     const D3 p00 = d3(p.cam.pixel00[0], p.cam.pixel00[1], p.cam.pixel00[2]);
     const D3 pxv = d3(p.cam.pixel_x[0], p.cam.pixel_x[1], p.cam.pixel_x[2]);
     const D3 pyv = d3(p.cam.pixel_y[0], p.cam.pixel_y[1], p.cam.pixel_y[2]);
     const D3 du = d3(p.cam.defocus_u[0], p.cam.defocus_u[1], p.cam.defocus_u[2]);
     const D3 dv = d3(p.cam.defocus_v[0], p.cam.defocus_v[1], p.cam.defocus_v[2]);
     const bool lens = p.cam.aperture > 0;
-    const D3 s0 = add(add(p00, smul(pxv, (double)x)), smul(pyv, y));
-    const D3 b0 = lens ? add(pos, smul(sub(s0, pos), p.focus_time)) : s0;
-    const double aa = p.spp > 1 ? p.ray_radius * __builtin_sqrt(length_sq(pxv) + length_sq(pyv)) : 0.0;
-    const double ra = lens ? __builtin_sqrt(length_sq(du) + length_sq(dv)) : 0.0;
-    const double rb = lens ? aa * __builtin_fabs(p.focus_time) : aa;
-    const D3 D = sub(b0, pos);
-    const double dn2 = length_sq(D), dn = __builtin_sqrt(dn2), L = ra + rb;
+    const D3 s0 = add(add(p00, smul(pxv, 0.5 * (xa + xb))), smul(pyv, 0.5 * (ya + yb)));
+    const D3 b0 = lens ? add(b.pos, smul(sub(s0, b.pos), p.focus_time)) : s0;
+    const double lx = __builtin_sqrt(length_sq(pxv)), ly = __builtin_sqrt(length_sq(pyv));
+    const double aa = (p.spp > 1 ? p.ray_radius * __builtin_sqrt(lx * lx + ly * ly) : 0.0) +
+                      0.5 * (xb - xa) * lx + 0.5 * (yb - ya) * ly;
+    b.ra = lens ? __builtin_sqrt(length_sq(du) + length_sq(dv)) : 0.0;
+    b.rb = lens ? aa * __builtin_fabs(p.focus_time) : aa;
+    b.D = sub(b0, b.pos);
+    b.dn2 = length_sq(b.D);
+    b.dn = __builtin_sqrt(b.dn2);
+    b.ok = b.dn > 2.0 * (b.ra + b.rb) && b.dn2 > 0;
+    b.scale = 1.0 + __builtin_fmax(__builtin_fmax(__builtin_fabs(b.pos.x), __builtin_fabs(b.pos.y)), __builtin_fabs(b.pos.z));
+    return b;
+}
+
+// Pass 1: one wave per 8x8 tile of compact pixels tests every tree sphere
+// (lane k: spheres k, k + 64, ...) against the tile's beam and keeps up to
+// kCandTileSlots of them in sphere order (else overflow: the tile's pixels test
+// every tree sphere).
+__global__ __launch_bounds__(256) void cand_tile_kernel(KernelParams p, uint16_t* lists, uint32_t* counts) {
+    const uint32_t tiles_x = ((uint32_t)p.width + 7u) / 8u, tiles_y = ((uint32_t)p.rows + 7u) / 8u;
+    const uint32_t t = blockIdx.x * 4u + threadIdx.x / 64u, lane = threadIdx.x & 63u;
+    if (t >= tiles_x * tiles_y) return;  // wave-uniform
+    const int32_t xa = (int32_t)(t % tiles_x) * 8, ja = (int32_t)(t / tiles_x) * 8;
+    const int32_t xb = min(xa + 7, p.width - 1), jb = min(ja + 7, p.rows - 1);
+    const Beam b = pixel_beam(p, (double)xa, (double)xb, (double)row_of(p, ja), (double)row_of(p, jb));
+    uint32_t n = 0;
+    const int32_t tree = p.n_slots - p.n_global;
+    for (int32_t s0 = 0; s0 < tree && b.ok && n <= kCandTileSlots; s0 += 64) {
+        const int32_t s = s0 + (int32_t)lane;
+        const bool hit = s < tree && beam_reaches(b.pos, b.D, b.dn2, b.dn, b.ra, b.rb, b.scale, p.bgeo[s],
+                                                   __builtin_fabs(p.bmat[s].radius));
+        const uint64_t m = __ballot(hit);
+        const uint32_t at = n + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (hit && at < kCandTileSlots) lists[(size_t)t * kCandTileSlots + at] = (uint16_t)s;
+        n += (uint32_t)__popcll(m);
+    }
+    if (lane == 0) counts[t] = b.ok && n <= kCandTileSlots ? n : kCandOverflow;
+}
+
+// Pass 2: one thread per compact pixel tests its tile's spheres (all tree
+// spheres when the tile overflowed) against the pixel's own beam.
+__global__ __launch_bounds__(256) void cand_build_kernel(KernelParams p, uint4* out, const uint16_t* lists,
+                                                        const uint32_t* counts) {
+    const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= (size_t)p.rows * (size_t)p.width) return;
+    const int32_t j = (int32_t)(i / (size_t)p.width), x = (int32_t)(i % (size_t)p.width);
+    const double y = (double)row_of(p, j);
+    const Beam b = pixel_beam(p, (double)x, (double)x, y, y);
+    const uint32_t tile = (uint32_t)(j / 8) * (((uint32_t)p.width + 7u) / 8u) + (uint32_t)(x / 8);
+    const uint32_t tn = counts[tile];
+    const bool all = tn == kCandOverflow;
+    const int32_t m = all ? p.n_slots - p.n_global : (int32_t)tn;
     uint32_t slots[kCandSlots];
     uint32_t n = 0;
-    bool ok = dn > 2.0 * L && dn2 > 0;
-    const double scale = 1.0 + __builtin_fmax(__builtin_fmax(__builtin_fabs(pos.x), __builtin_fabs(pos.y)), __builtin_fabs(pos.z));
-    const int32_t tree = p.n_slots - p.n_global;  // slots of the tree's spheres
-    for (int32_t s = 0; s < tree && ok; ++s) {
-        const double4 g = p.bgeo[s];
-        const double R = __builtin_fabs(p.bmat[s].radius);
-        const D3 rel = sub(d3(g.x, g.y, g.z), pos);
-        const double tc = dot(rel, D) / dn2;
-        const double tcl = __builtin_fmax(tc, 0.0);
-        const double dperp = __builtin_sqrt(length_sq(sub(rel, smul(D, tc))));
-        const double margin = 1e-6 * (scale + __builtin_fabs(g.x) + __builtin_fabs(g.y) + __builtin_fabs(g.z) + R);
-        const double reach = R + __builtin_fabs(1.0 - tcl) * ra + tcl * rb + margin;
-        if (dperp <= reach + L * reach / (dn - L) + margin || !(dperp == dperp)) {
+    bool ok = b.ok;
+    for (int32_t k = 0; k < m && ok; ++k) {
+        const int32_t s = all ? k : (int32_t)lists[(size_t)tile * kCandTileSlots + k];
+        if (beam_reaches(b.pos, b.D, b.dn2, b.dn, b.ra, b.rb, b.scale, p.bgeo[s], __builtin_fabs(p.bmat[s].radius))) {
             if (n == kCandSlots) ok = false;
             else slots[n++] = (uint32_t)s;
         }
@@ -1407,10 +1464,23 @@ __global__ __launch_bounds__(256) void cand_build_kernel(KernelParams p, uint4* 
     out[i] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+size_t cand_workspace_bytes(int32_t width, int32_t rows) {
+    const size_t pixels = (size_t)rows * (size_t)width;
+    const size_t tiles = (size_t)((width + 7) / 8) * (size_t)((rows + 7) / 8);
+    return pixels * sizeof(uint4) + tiles * (kCandTileSlots * sizeof(uint16_t) + sizeof(uint32_t));
+}
+
 hipError_t launch_cand_build(const KernelParams& p, uint4* out, hipStream_t stream) {
     const size_t n = (size_t)p.rows * (size_t)p.width;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(cand_build_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, p, out);
+    const size_t tiles = (size_t)((p.width + 7) / 8) * (size_t)((p.rows + 7) / 8);
+    uint16_t* lists = reinterpret_cast<uint16_t*>(out + n);
+    uint32_t* counts = reinterpret_cast<uint32_t*>(lists + tiles * kCandTileSlots);
+    hipLaunchKernelGGL(cand_tile_kernel, dim3((uint32_t)((tiles + 3) / 4)), dim3(256), 0, stream, p, lists, counts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(cand_build_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, p, out, lists,
+                       counts);
     return hipGetLastError();
 }
 

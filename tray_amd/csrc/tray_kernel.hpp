@@ -112,11 +112,16 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
 // tree spheres (leaf slots) that any camera ray of the pixel can reach, by a
 // conservative bound on the beam from the lens disc through the pixel's
 // anti-aliasing disc; a record holds up to kCandSlots slots, or
-// kCandOverflow (that pixel's camera rays traverse the BVH). `out` holds
-// rows x width records. Needs p's camera, image, row, BVH geometry and shading
-// record fields.
+// kCandOverflow (that pixel's camera rays traverse the BVH). Needs p's camera,
+// image, row, BVH geometry and shading record fields.
+// The build runs in two passes: 8x8 tiles of pixels first (up to
+// kCandTileSlots spheres per tile), then each pixel over its tile's list;
+// `out` must hold cand_workspace_bytes(width, rows) (the records, then the
+// tile lists).
 constexpr uint32_t kCandSlots = 7;
+constexpr uint32_t kCandTileSlots = 64;
 constexpr uint32_t kCandOverflow = 0xFFFFu;
+size_t cand_workspace_bytes(int32_t width, int32_t rows);
 hipError_t launch_cand_build(const KernelParams& p, uint4* out, hipStream_t stream);
 
 // ColorF.ToSRGBA over n device pixels (3 doubles each) into RGBA8 words, with the
