@@ -303,6 +303,9 @@ struct Stats {
 #ifdef TRAY_STATS_PRIMARY  // diagnostic: node visits, leaf visits, box tests of primary segments; all node/leaf visits
     uint64_t nodes0 = 0, leaves0 = 0, boxes0 = 0, nodes = 0, leaves = 0;
 #endif
+#ifdef TRAY_STATS_GROUND  // diagnostic: segments leaving an out-of-tree sphere (upward cube face / any) and their visits
+    uint64_t g_seg[2] = {0, 0}, g_nodes[2] = {0, 0}, g_leaves[2] = {0, 0}, nodes = 0, leaves = 0;
+#endif
 };
 #else  // phase profiles count in LDS; per-lane counters would cost registers
 struct NoCount {
@@ -1040,6 +1043,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     T.cur = kBvhNone;  // idle
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
     bool exhausted = false;
+#ifdef TRAY_STATS_GROUND
+    uint32_t gcls = 0;  // diagnostic: class of the lane's current segment (1/2: from an out-of-tree sphere, up / other)
+#endif
     int32_t prog_cur = 0;  // live progress: the wave's current tile row and its unflushed count
     uint32_t prog_cnt = 0;
 #ifdef TRAY_PROFILE
@@ -1097,6 +1103,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 if constexpr (kBVH)
                     if (p.cand) cand = p.cand[(size_t)j * (size_t)p.width + (size_t)x];
                 start_sample(p, uni, L, fresh_item, x, j, (p.pass0 + pass) * (uint32_t)p.spp + smp);
+#ifdef TRAY_STATS_GROUND
+                gcls = 0;
+#endif
                 if constexpr (kBVH) {
                     ++L.segments;
                     T.tlim = __builtin_inff();
@@ -1164,6 +1173,13 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                             if (L.bounce == 0) ++st.nodes0, st.boxes0 += tested;
                         }
 #endif
+#if defined(TRAY_STATS_GROUND) && !defined(TRAY_PROFILE)
+                        if constexpr (kStats) {
+                            ++st.nodes;
+                            if (gcls == 1) ++st.g_nodes[0];
+                            if (gcls != 0) ++st.g_nodes[1];
+                        }
+#endif
                     }
                 }
                 PROF_ADD(1);
@@ -1188,6 +1204,13 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         if (L.bounce == 0) ++st.leaves0;
                     }
 #endif
+#if defined(TRAY_STATS_GROUND) && !defined(TRAY_PROFILE)
+                    if constexpr (kStats) {
+                        ++st.leaves;
+                        if (gcls == 1) ++st.g_leaves[0];
+                        if (gcls != 0) ++st.g_leaves[1];
+                    }
+#endif
                 }
                 PROF_ADD(2);
             }
@@ -1208,6 +1231,17 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     if (shade_step<kStats>(p, uni, L, T.best, T.closest, T.a, [&] { return sv.bgeo[T.slot]; },
                                            [&] { return sv.bmat[T.slot]; }, st)) {
                         ++L.segments;
+#if defined(TRAY_STATS_GROUND) && !defined(TRAY_PROFILE)
+                        {
+                            const bool from_g = T.best >= 0 && T.slot >= sv.global_first;
+                            const bool up = L.dir.y >= __builtin_fmax(__builtin_fabs(L.dir.x), __builtin_fabs(L.dir.z));
+                            gcls = from_g ? (up ? 1u : 2u) : 0u;
+                            if constexpr (kStats) {
+                                if (gcls == 1) ++st.g_seg[0];
+                                if (gcls != 0) ++st.g_seg[1];
+                            }
+                        }
+#endif
                         trav_begin(T, sv, L.org, L.dir);
                         if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
                     } else {
@@ -1230,6 +1264,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         atomicAdd(p.stats + 5, (unsigned long long)st.boxes0);
         atomicAdd(p.stats + 6, (unsigned long long)st.nodes);
         atomicAdd(p.stats + 7, (unsigned long long)st.leaves);
+#endif
+#if defined(TRAY_STATS_GROUND) && !defined(TRAY_PROFILE)
+        for (int k = 0; k < 2; ++k) {
+            atomicAdd(p.stats + 3 + k, (unsigned long long)st.g_seg[k]);
+            atomicAdd(p.stats + 5 + k, (unsigned long long)st.g_nodes[k]);
+            atomicAdd(p.stats + 7 + k, (unsigned long long)st.g_leaves[k]);
+        }
+        atomicAdd(p.stats + 9, (unsigned long long)st.nodes);
+        atomicAdd(p.stats + 10, (unsigned long long)st.leaves);
 #endif
     }
 #ifdef TRAY_PROFILE
@@ -1691,6 +1734,8 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         e = hipMemsetAsync(p.stats, 0, 19 * sizeof(unsigned long long), stream);
 #elif defined(TRAY_STATS_PRIMARY)
         e = hipMemsetAsync(p.stats, 0, 8 * sizeof(unsigned long long), stream);
+#elif defined(TRAY_STATS_GROUND)
+        e = hipMemsetAsync(p.stats, 0, 11 * sizeof(unsigned long long), stream);
 #else
         e = hipMemsetAsync(p.stats, 0, 3 * sizeof(unsigned long long), stream);
 #endif
