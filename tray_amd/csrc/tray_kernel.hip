@@ -893,7 +893,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #define TRAY_NODE_MORE_LANES 64
 #endif
 #ifndef TRAY_LEAF_BATCH
-#define TRAY_LEAF_BATCH 24
+#define TRAY_LEAF_BATCH 20
 #endif
 #ifndef TRAY_SHADE_BATCH
 #define TRAY_SHADE_BATCH 40
@@ -901,6 +901,11 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 // Idle lanes are refilled (a camera ray each) once this many wait, or the whole wave does.
 #ifndef TRAY_REFILL_BATCH
 #define TRAY_REFILL_BATCH 24
+#endif
+// Camera rays answered by their candidate list are shaded inside the refill phase (1) or wait for
+// the shade phase (0).
+#ifndef TRAY_REFILL_SHADE
+#define TRAY_REFILL_SHADE 1
 #endif
 
 // Cost probes (diagnostic builds only, never timed as the product): N extra
@@ -1065,6 +1070,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         // Items are assigned first (cheap, may span two chunks); the camera rays of
         // all newly assigned lanes are then generated together.
         uint32_t fresh_item = ~0u;
+        bool cam_hit = false;  // a camera ray whose Scene.Hit the candidate list answered in this refill
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
                 const uint32_t c = take_chunk(p, uni, lane);
@@ -1125,12 +1131,36 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         }
                         if constexpr (kStats) st.spheres += n_cand;
                         T.cur = kBvhNone;  // traversal done: the lane waits for the shade phase
+                        cam_hit = true;
                     } else {
                         trav_begin32(T, sv, L.org, L.dir);
                     }
                 }
             }
         }
+#if TRAY_REFILL_SHADE
+        // The refill's camera rays with a known hit are shaded at once (their
+        // scattered rays join the node steps below) instead of waiting for the
+        // shade batch; the traversal lanes' batching is unchanged.
+        if constexpr (kBVH) {
+            if (__ballot(cam_hit) != 0ull) {
+                bool ended = false;
+                if (cam_hit) {
+                    if (shade_step<kStats>(p, uni, L, T.best, T.closest, T.a, [&] { return sv.bgeo[T.slot]; },
+                                           [&] { return sv.bmat[T.slot]; }, st)) {
+                        ++L.segments;
+                        trav_begin(T, sv, L.org, L.dir);
+                        if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
+                    } else {
+                        ended = true;
+                    }
+                }
+                if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
+            }
+        }
+#else
+        (void)cam_hit;
+#endif
         PROF_ADD(0);
         if (__ballot(L.busy) == 0ull) {
             if (exhausted) break;
