@@ -902,6 +902,17 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #ifndef TRAY_REFILL_BATCH
 #define TRAY_REFILL_BATCH 24
 #endif
+// Below TRAY_TRAV_SPARSE traversing lanes (node steps mostly empty) the leaf and shade phases
+// already run from TRAY_LEAF_LOW / TRAY_SHADE_LOW waiting lanes (TRAY_SHADE_LOW 64: shade batches unchanged).
+#ifndef TRAY_TRAV_SPARSE
+#define TRAY_TRAV_SPARSE 8
+#endif
+#ifndef TRAY_LEAF_LOW
+#define TRAY_LEAF_LOW 8
+#endif
+#ifndef TRAY_SHADE_LOW
+#define TRAY_SHADE_LOW 64
+#endif
 // Camera rays answered by their candidate list are shaded inside the refill phase (1) or wait for
 // the shade phase (0).
 #ifndef TRAY_REFILL_SHADE
@@ -1216,8 +1227,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             }
             // Leaf phase: FP64 sphere tests, batched.
             const uint64_t m_leaf = __ballot(is_leaf(T.cur));
-            if (m_leaf != 0ull &&
-                (__popcll(m_leaf) >= TRAY_LEAF_BATCH || __ballot(is_trav(T.cur)) == 0ull)) {
+            const uint32_t n_trav = (uint32_t)__popcll(__ballot(is_trav(T.cur)));
+            if (m_leaf != 0ull && (__popcll(m_leaf) >= TRAY_LEAF_BATCH || n_trav == 0u ||
+                                   (n_trav < TRAY_TRAV_SPARSE && __popcll(m_leaf) >= TRAY_LEAF_LOW))) {
                 PROF_T0();
                 PROF_CNT(6, 1);
                 PROF_CNT(7, __popcll(m_leaf));
@@ -1246,7 +1258,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             }
             // Shading phase, batched.
             const uint64_t m_shade = __ballot(L.busy && T.cur == kBvhNone);
-            if (m_shade != 0ull && (__popcll(m_shade) >= TRAY_SHADE_BATCH || __ballot(T.cur < kBvhNone) == 0ull)) {
+            if (m_shade != 0ull && (__popcll(m_shade) >= TRAY_SHADE_BATCH || __ballot(T.cur < kBvhNone) == 0ull ||
+                                    (__popcll(__ballot(is_trav(T.cur))) < TRAY_TRAV_SPARSE &&
+                                     __popcll(m_shade) >= TRAY_SHADE_LOW))) {
                 PROF_T0();
                 PROF_CNT(8, 1);
                 PROF_CNT(9, __popcll(m_shade));
