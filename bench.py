@@ -12,7 +12,7 @@ collective inside the render) and the frames are gathered to rank 0 by RCCL
 over xGMI ("scaling": "strong": the frame is fixed as N grows).
 value = W*H*r*steps / max-over-ranks wall time.
 Frames are progressive passes (tray_params.pass = frame index: every frame
-draws fresh samples). --passes F (default 8, THE SAME AT EVERY N, so the N = 1
+draws fresh samples). --passes F (default 16, THE SAME AT EVERY N, so the N = 1
 line and every point of a 1 -> 8 curve share one launch shape) renders F
 frames per launch (tray_render_passes_async: lanes flow from one frame's
 samples into the next, so a launch has one tail of long paths, not F); at
@@ -119,7 +119,7 @@ def main() -> int:
     ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="launches overlap this deep (own scene copy, output and stream each): a launch's "
                          "blocks start on CUs the previous launch's last paths leave idle")
-    ap.add_argument("--passes", type=int, default=8,
+    ap.add_argument("--passes", type=int, default=16,
                     help="frames per launch, the same at every N (tray_render_passes_async: consecutive "
                          "progressive passes in one persistent launch, one tail of long paths per launch)")
     args = ap.parse_args()

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 TOL, TIGHT = 1e-4, 1e-12
 WORKERS = min(16, os.cpu_count() or 4)
-MAX_BAND_SAMPLES = 1 << 29  # tray_kernel.hpp kMaxBandSamples
+MAX_BAND_SAMPLES = 1 << 30  # tray_kernel.hpp kMaxBandSamples
 
 
 def band_rows(W, spp):

@@ -5,7 +5,7 @@
 #   usage: tools/profile_bench.sh <outdir> [bench.py args...]
 set -u
 OUT=${1:-gpurun_out/prof}; shift || true
-ARGS=${*:-"--steps 8 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"}
+ARGS=${*:-"--steps 16 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py $ARGS > "$OUT/kt.log" 2>&1 || exit 1

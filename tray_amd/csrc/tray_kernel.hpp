@@ -132,7 +132,10 @@ hipError_t launch_to_srgba(const double* rgb, size_t n_pixels, uint32_t* rgba, c
 
 // Samples per launch band (the sample buffer holds one band: 24 B per sample);
 // the TRAY_BAND_SAMPLES environment variable lowers it (tests exercise bands).
-constexpr uint64_t kMaxBandSamples = 1ull << 29;  // 12.9 GB of sample buffer (of 288 GB of HBM)
+#ifndef TRAY_BAND_LOG2
+#define TRAY_BAND_LOG2 30
+#endif
+constexpr uint64_t kMaxBandSamples = 1ull << TRAY_BAND_LOG2;  // 2^30: 25.8 GB of sample buffer (of 288 GB of HBM)
 uint64_t max_band_samples();
 // Bytes of sample buffer launch_render needs for `rows` compact rows.
 size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp);
