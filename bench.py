@@ -106,8 +106,8 @@ def _profile_json(name, config, frames):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--tile-rows", type=int, default=1, help="rows per interleaved tile (N > 1): 1 balances best")
     ap.add_argument("--no-cpu-baseline", action="store_true")
