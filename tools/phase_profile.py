@@ -20,6 +20,7 @@ def main():
     ap.add_argument("lib")
     ap.add_argument("--config", default="c2")
     ap.add_argument("--shard", default=None, help="N,K: rank K's row tiles of an N-way split (1-row tiles)")
+    ap.add_argument("--refill-split", action="store_true", help="the library is a -DTRAY_PROFILE_REFILL build")
     ap.add_argument("--waves", type=int, default=256 * 16, help="waves in the launch (CUs x waves per CU)")
     args = ap.parse_args()
     import torch
@@ -44,12 +45,17 @@ def main():
     torch.cuda.synchronize()
     allv = stats.tolist()
     v = allv[:22]
+    # -DTRAY_PROFILE_REFILL: stats[13], [16], [17], [18] (slots 10, 13-15) hold the refill split
+    refill_split = dict(zip(["refill_assign", "refill_camera", "refill_hit", "refill_shade"],
+                            [allv[13], allv[16], allv[17], allv[18]]))
     se = allv[32:]
     names = ["segments", "sphere_tests", "box_tests", "cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade",
              "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "node_leafwait_lanes", "node_shadewait_lanes", "refill_phases", "refill_lanes",
              "unused_15", "rt_end_max", "rt_life_sum",
              "rt_start_min_inv"]
     d = dict(zip(names, v))
+    if args.refill_split:
+        d["refill_split_share"] = {k: round(x / max(1, d["cyc_refill"]), 3) for k, x in refill_split.items()}
     cyc = sum(d[k] for k in PHASES)
     d["share"] = {k: round(d[k] / cyc, 3) for k in PHASES}
     d["lanes_per_node_iter"] = round(d["node_lanes"] / max(1, d["node_iters"]), 1)

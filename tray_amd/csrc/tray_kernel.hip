@@ -1073,7 +1073,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #endif
 
     while (true) {
+#ifndef TRAY_PROFILE_REFILL  // slots 10, 13-15 hold the refill split instead
         PROF_CNT(10, 1);
+#endif
         // Refill idle lanes from the wave's pool, fetching 64-item chunks from the global queue.
         PROF_T0();
         uint64_t idle = __ballot(!L.busy);
@@ -1082,6 +1084,12 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         // all newly assigned lanes are then generated together.
         uint32_t fresh_item = ~0u;
         bool cam_hit = false;  // a camera ray whose Scene.Hit the candidate list answered in this refill
+#ifdef TRAY_PROFILE_CANDWAIT
+        uint64_t prof_wait = 0;
+#endif
+#ifdef TRAY_PROFILE_REFILL
+        uint64_t prof_cam = 0, prof_hit = 0;  // stamps after the camera ray / after its Scene.Hit
+#endif
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
                 const uint32_t c = take_chunk(p, uni, lane);
@@ -1101,12 +1109,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             pool_next += take;
             idle = __ballot(!L.busy && fresh_item == ~0u);
         }
-#ifdef TRAY_PROFILE
+#if defined(TRAY_PROFILE) && !defined(TRAY_PROFILE_REFILL)
         {
             const uint64_t fresh = __ballot(fresh_item != ~0u);
             PROF_CNT(13, fresh != 0ull ? 1 : 0);
             PROF_CNT(14, __popcll(fresh));
         }
+#endif
+#ifdef TRAY_PROFILE_REFILL
+        const uint64_t prof_assigned = __builtin_amdgcn_s_memtime();
 #endif
         if (fresh_item != ~0u) {
             int32_t x, j;
@@ -1120,8 +1131,18 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 if constexpr (kBVH)
                     if (p.cand) cand = p.cand[(size_t)j * (size_t)p.width + (size_t)x];
                 start_sample(p, uni, L, fresh_item, x, j, (p.pass0 + pass) * (uint32_t)p.spp + smp);
+#ifdef TRAY_PROFILE_REFILL
+                prof_cam = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef TRAY_STATS_GROUND
                 gcls = 0;
+#endif
+#ifdef TRAY_PROFILE_CANDWAIT
+                {  // diagnostic: the candidate record's exposed latency after the camera ray
+                    const uint64_t w0 = __builtin_amdgcn_s_memtime();
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                    prof_wait = __builtin_amdgcn_s_memtime() - w0 + 1u;
+                }
 #endif
                 if constexpr (kBVH) {
                     ++L.segments;
@@ -1147,8 +1168,14 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         trav_begin32(T, sv, L.org, L.dir);
                     }
                 }
+#ifdef TRAY_PROFILE_REFILL
+                prof_hit = __builtin_amdgcn_s_memtime();
+#endif
             }
         }
+#ifdef TRAY_PROFILE_REFILL
+        const uint64_t prof_shade0 = __builtin_amdgcn_s_memtime();
+#endif
 #if TRAY_REFILL_SHADE
         // The refill's camera rays with a known hit are shaded at once (their
         // scattered rays join the node steps below) instead of waiting for the
@@ -1171,6 +1198,34 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         }
 #else
         (void)cam_hit;
+#endif
+#ifdef TRAY_PROFILE_REFILL
+        {
+            const uint64_t prof_shade1 = __builtin_amdgcn_s_memtime();
+            PROF_CNT(10, prof_assigned - prof_t0_);  // item assignment (pool, queue)
+            PROF_CNT(15, prof_shade1 - prof_shade0);  // shading of the candidate-answered camera rays
+            const uint64_t mw = __ballot(prof_cam != 0u);
+            if (mw != 0ull) {
+                const uint32_t lw = (uint32_t)__builtin_ctzll(mw);
+                const uint64_t c = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(prof_cam >> 32), lw) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((uint32_t)prof_cam, lw);
+                const uint64_t h = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(prof_hit >> 32), lw) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((uint32_t)prof_hit, lw);
+                PROF_CNT(13, c - prof_assigned);  // decoding + camera ray (Philox, discs)
+                PROF_CNT(14, h - c);              // out-of-tree spheres + candidates (or the FP32 setup)
+            }
+        }
+#endif
+#ifdef TRAY_PROFILE_CANDWAIT
+        {
+            const uint64_t mw = __ballot(prof_wait != 0u);
+            if (mw != 0ull) {
+                const uint32_t lw = (uint32_t)__builtin_ctzll(mw);
+                const uint64_t w = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(prof_wait >> 32), lw) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((uint32_t)prof_wait, lw);
+                PROF_CNT(15, w - 1u);
+            }
+        }
 #endif
         PROF_ADD(0);
         if (__ballot(L.busy) == 0ull) {
