@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
-"""Where the cold synchronous render's extra time goes (C2): scene upload
-(BVH build + copies), the first render of a fresh scene (sample-buffer
-allocation), a warm render, and the host copy. Diagnostic only.
+"""Where a synchronous drop-in Render's time goes (bench.py `e2e`): host-timed
+pieces of a C2 render with a scene the device has not seen — the scene upload
+(BVH build + copies), the first launch on it (sample-buffer allocation,
+candidate build), a warm launch, and the whole synchronous tray_render call
+with a new scene and with the cached one. Median of --reps runs, milliseconds;
+`render_first_at_size` is the process's first render at this size (what
+bench.py's `e2e_ms_new_scene` measures).
 
-    python tools/e2e_breakdown.py
+    python tools/e2e_breakdown.py [--config c2] [--reps 5]
 """
+import argparse
 import json
 import os
 import sys
@@ -15,42 +20,52 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import numpy as np
     import torch
 
     from bench import CONFIGS
     from tray_amd import _lib, ray
 
-    _, seed, half, W, H, spp, depth = CONFIGS["c2"]
-    spheres = ray.rich_scene_array(seed, half)
+    label, seed, half, W, H, spp, depth = CONFIGS[args.config]
+    base = ray.rich_scene_array(seed, half)
     cam = ray.RichSceneCamera()
     cam.Initialize(W, H)
     bg = ray._background(ray.DefaultBackground())
     p = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGBA8)
     out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
-    warm = _lib.DeviceScene(spheres, bg, 0)  # loads the code object, first launch
-    warm.render_async(cam._state, p, out.data_ptr())
-    torch.cuda.synchronize()
-    rec = {}
-    t0 = time.perf_counter()
-    sc = _lib.DeviceScene(spheres, bg, 0)
-    rec["scene_upload_ms"] = (time.perf_counter() - t0) * 1e3
-    t0 = time.perf_counter()
-    sc.render_async(cam._state, p, out.data_ptr())
-    torch.cuda.synchronize()
-    rec["first_render_ms"] = (time.perf_counter() - t0) * 1e3
-    t0 = time.perf_counter()
-    sc.render_async(cam._state, p, out.data_ptr())
-    torch.cuda.synchronize()
-    rec["warm_render_ms"] = (time.perf_counter() - t0) * 1e3
-    t0 = time.perf_counter()
-    host = out.cpu()
-    rec["d2h_pageable_ms"] = (time.perf_counter() - t0) * 1e3
-    for k in range(3):
+    stream = torch.cuda.current_stream()
+    _lib.render(ray.DefaultScene().to_array(), bg, cam._state, _lib.make_params(8, 8, 4, 1, 0.5, seed))  # runtime setup
+
+    def fresh(k):  # a scene no cache has seen (k >= -1): one sphere nudged
+        s = base.copy()
+        s["center"][1][0] += 1e-9 * (k + 2)
+        return s
+
+    def ms(f):
         t0 = time.perf_counter()
-        _lib.render(spheres, bg, cam._state, p)
-        rec[f"tray_render_{k}_ms"] = (time.perf_counter() - t0) * 1e3
-    print(json.dumps({k: round(v, 3) for k, v in rec.items()}))
-    del host
+        r = f()
+        return (time.perf_counter() - t0) * 1e3, r
+
+    first_at_size, _ = ms(lambda: _lib.render(fresh(-1), bg, cam._state, p))  # bench.py's e2e_ms_new_scene
+    rows = {"upload": [], "first_launch": [], "warm_launch": [], "render_new_scene": [], "render_cached": []}
+    for k in range(args.reps):
+        t, sc = ms(lambda: _lib.DeviceScene(fresh(2 * k), bg))
+        rows["upload"].append(t)
+        for key in ("first_launch", "warm_launch"):
+            def go():
+                sc.render_async(cam._state, p, out.data_ptr(), None, stream.cuda_stream)
+                torch.cuda.synchronize()
+            rows[key].append(ms(go)[0])
+        sc.release()
+        s = fresh(2 * k + 1)
+        rows["render_new_scene"].append(ms(lambda: _lib.render(s, bg, cam._state, p))[0])
+        rows["render_cached"].append(ms(lambda: _lib.render(s, bg, cam._state, p))[0])
+    print(json.dumps({"config": args.config, "reps": args.reps, "render_first_at_size": round(first_at_size, 3),
+                      **{k: round(float(np.median(v)), 3) for k, v in rows.items()}}))
 
 
 if __name__ == "__main__":

@@ -141,6 +141,9 @@ struct tray_scene_s {
     double4* bgeo;
     int32_t* bidx;
     tray::MatRec* bmat;
+    // One device allocation holds geo, mat, queue, srgb and the BVH arrays (the
+    // pointers above point into it); stack_ovf, samples and cand are separate.
+    void* arena;
     // Per-sample path colours of one launch band (tray_kernel.hpp), grown on
     // demand: renders of one scene must be ordered (one stream, or synchronised).
     double* samples;
@@ -325,44 +328,50 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->queue = nullptr;
     sc->bg_a = V3{bg->color_a[0], bg->color_a[1], bg->color_a[2]};
     sc->bg_b = V3{bg->color_b[0], bg->color_b[1], bg->color_b[2]};
-    hipError_t e = hipMalloc(&sc->geo, sizeof(double4) * (size_t)n_pad);
-    if (e == hipSuccess) e = hipMalloc(&sc->queue, sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemset(sc->queue, 0, sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemcpy(sc->geo, geo.data(), sizeof(double4) * (size_t)n_pad, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&sc->srgb, 256 * sizeof(double));
-    if (e == hipSuccess) e = hipMemcpy(sc->srgb, srgb_thresholds(), 256 * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess && n > 0) e = hipMalloc(&sc->mat, sizeof(MatRec) * (size_t)n);
-    if (e == hipSuccess && n > 0) e = hipMemcpy(sc->mat, mat.data(), sizeof(MatRec) * (size_t)n, hipMemcpyHostToDevice);
+    // One arena, filled from one host image with one copy: eleven allocations
+    // and seven synchronous copies took the C2 upload from 0.31 to 0.44 ms
+    // (tools/e2e_breakdown.py, profiles/r2g_e2e_breakdown.jsonl).
+    struct Part {
+        void** dst;
+        const void* src;  // nullptr: zeros
+        size_t bytes;
+    };
+    const Part parts[] = {
+        {(void**)&sc->geo, geo.data(), sizeof(double4) * (size_t)n_pad},
+        {(void**)&sc->queue, nullptr, sizeof(uint32_t)},
+        {(void**)&sc->srgb, srgb_thresholds(), 256 * sizeof(double)},
+        {(void**)&sc->mat, mat.data(), sizeof(MatRec) * (size_t)n},
+        {(void**)&sc->nodes, bvh.nodes.data(), has_bvh ? sizeof(Bvh4Node) * bvh.nodes.size() : 0},
+        {(void**)&sc->leaves, bvh.leaves.data(), has_bvh ? sizeof(int32_t) * bvh.leaves.size() : 0},
+        {(void**)&sc->bgeo, bvh.geo.data(), has_bvh ? sizeof(double4) * bvh.geo.size() : 0},
+        {(void**)&sc->bidx, bvh.idx.data(), has_bvh ? sizeof(int32_t) * bvh.idx.size() : 0},
+        {(void**)&sc->bmat, bmat.data(), has_bvh ? sizeof(MatRec) * bmat.size() : 0},
+    };
+    constexpr size_t kAlign = 256;
+    size_t total = 0;
+    for (const Part& q : parts) total += (q.bytes + kAlign - 1) / kAlign * kAlign;
+    std::vector<uint8_t> image(total, 0);
+    size_t at = 0;
+    std::vector<size_t> offsets;
+    for (const Part& q : parts) {
+        offsets.push_back(at);
+        if (q.src && q.bytes) memcpy(image.data() + at, q.src, q.bytes);
+        at += (q.bytes + kAlign - 1) / kAlign * kAlign;
+    }
+    sc->arena = nullptr;
+    hipError_t e = hipMalloc(&sc->arena, total);
+    if (e == hipSuccess) e = hipMemcpy(sc->arena, image.data(), total, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        for (size_t i = 0; i < sizeof(parts) / sizeof(parts[0]); ++i)  // empty arrays stay null
+            *parts[i].dst = parts[i].bytes ? static_cast<uint8_t*>(sc->arena) + offsets[i] : nullptr;
+    }
     if (e == hipSuccess && has_bvh) {
-        e = hipMalloc(&sc->nodes, sizeof(Bvh4Node) * bvh.nodes.size());
         const size_t ovf = bvh_stack_overflow_bytes(bvh.stack_max + kStackSlack, device);
-        if (e == hipSuccess && ovf) e = hipMalloc(&sc->stack_ovf, ovf);
-        if (e == hipSuccess) e = hipMalloc(&sc->leaves, sizeof(int32_t) * bvh.leaves.size());
-        if (e == hipSuccess)
-            e = hipMemcpy(sc->leaves, bvh.leaves.data(), sizeof(int32_t) * bvh.leaves.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMalloc(&sc->bgeo, sizeof(double4) * bvh.geo.size());
-        if (e == hipSuccess) e = hipMalloc(&sc->bidx, sizeof(int32_t) * bvh.idx.size());
-        if (e == hipSuccess)
-            e = hipMemcpy(sc->nodes, bvh.nodes.data(), sizeof(Bvh4Node) * bvh.nodes.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(sc->bgeo, bvh.geo.data(), sizeof(double4) * bvh.geo.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(sc->bidx, bvh.idx.data(), sizeof(int32_t) * bvh.idx.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMalloc(&sc->bmat, sizeof(MatRec) * bmat.size());
-        if (e == hipSuccess)
-            e = hipMemcpy(sc->bmat, bmat.data(), sizeof(MatRec) * bmat.size(), hipMemcpyHostToDevice);
+        if (ovf) e = hipMalloc(&sc->stack_ovf, ovf);
     }
     if (e != hipSuccess) {
-        (void)hipFree(sc->geo);
-        (void)hipFree(sc->mat);
-        (void)hipFree(sc->queue);
-        (void)hipFree(sc->nodes);
-        (void)hipFree(sc->leaves);
+        (void)hipFree(sc->arena);
         (void)hipFree(sc->stack_ovf);
-        (void)hipFree(sc->bgeo);
-        (void)hipFree(sc->bidx);
-        (void)hipFree(sc->bmat);
-        (void)hipFree(sc->srgb);
         delete sc;
         return hip_fail(e, "scene upload");
     }
@@ -388,17 +397,9 @@ int tray_scene_get_info(tray_scene_t sc, tray_scene_info* out) {
 int tray_scene_release(tray_scene_t sc) {
     if (!sc) return TRAY_OK;
     (void)hipSetDevice(sc->device);
-    if (sc->geo) (void)hipFree(sc->geo);
-    if (sc->mat) (void)hipFree(sc->mat);
-    if (sc->queue) (void)hipFree(sc->queue);
-    if (sc->nodes) (void)hipFree(sc->nodes);
-    if (sc->leaves) (void)hipFree(sc->leaves);
+    if (sc->arena) (void)hipFree(sc->arena);
     if (sc->stack_ovf) (void)hipFree(sc->stack_ovf);
-    if (sc->bgeo) (void)hipFree(sc->bgeo);
-    if (sc->bidx) (void)hipFree(sc->bidx);
-    if (sc->bmat) (void)hipFree(sc->bmat);
     if (sc->samples) (void)hipFree(sc->samples);
-    if (sc->srgb) (void)hipFree(sc->srgb);
     if (sc->cand) (void)hipFree(sc->cand);
     delete sc;
     return TRAY_OK;
@@ -567,12 +568,27 @@ static int cached_scene(Slot& sl, const tray_sphere* spheres, int32_t n, const t
                       (n == 0 || memcmp(sl.cached_spheres.data(), spheres, sizeof(tray_sphere) * (size_t)n) == 0) &&
                       memcmp(&sl.cached_bg, bg, sizeof(*bg)) == 0;
     if (!same) {
-        if (sl.cached) tray_scene_release(sl.cached);
+        tray_scene_t old = sl.cached;
         sl.cached = nullptr;
         sl.cached_spheres.clear();
         tray_scene_t sc = nullptr;
         const int rc = tray_scene_upload(spheres, n, bg, device, &sc);
-        if (rc) return rc;
+        if (rc) {
+            if (old) tray_scene_release(old);
+            return rc;
+        }
+        if (old) {
+            // The slot's renders are synchronous, so the old scene's sample and
+            // candidate buffers are idle: the new scene takes them over instead of
+            // allocating its own (a C2 frame's 1.4-GB sample buffer: 0.28 ms of
+            // hipFree + hipMalloc per new scene, profiles/r2g_e2e_breakdown.jsonl).
+            std::swap(sc->samples, old->samples);
+            std::swap(sc->samples_bytes, old->samples_bytes);
+            std::swap(sc->cand, old->cand);
+            std::swap(sc->cand_bytes, old->cand_bytes);
+            sc->cand_valid = false;
+            tray_scene_release(old);
+        }
         sl.cached = sc;
         if (n > 0) sl.cached_spheres.assign(spheres, spheres + n);
         sl.cached_bg = *bg;
