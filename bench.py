@@ -349,7 +349,9 @@ def e2e_timings(_lib, spheres, bg, cam, W, H, depth, spp, seed):
     buffer; tools/hip_setup_costs.hip measures ~8 ms each). `e2e_ms_new_scene`:
     the next call, with the config's scene not yet on the device (BVH build,
     upload, sample-buffer allocation, render, copy). `e2e_ms`: the same scene
-    again (the library keeps the last scene it uploaded), median of 3."""
+    again (the library keeps the last scene it uploaded), median of 3.
+    `e2e_ms_new_scene_warm`: three more scenes the device has not seen (one
+    sphere nudged), median: a new scene once the buffers exist."""
     import numpy as np
 
     from tray_amd import ray
@@ -365,9 +367,18 @@ def e2e_timings(_lib, spheres, bg, cam, W, H, depth, spp, seed):
         _lib.render(spheres, bg, cam._state, p)
         ts.append((time.perf_counter() - t0) * 1e3)
     warm = float(np.median(ts[1:]))
+    news = []
+    for k in range(3):  # scenes the process has not seen, after it has rendered at this size
+        other = np.array(spheres, copy=True)
+        other["center"][-1][0] += 1e-9 * (k + 1)
+        t0 = time.perf_counter()
+        _lib.render(other, bg, cam._state, p)
+        news.append((time.perf_counter() - t0) * 1e3)
     return {"first_call_ms": round(first, 3), "e2e_ms_new_scene": round(ts[0], 3), "e2e_ms": round(warm, 3),
+            "e2e_ms_new_scene_warm": round(float(np.median(news)), 3),
             "e2e_mrays": round(W * H * spp / warm / 1e3, 1),
-            "what": "tray_render, RGBA8 into host memory; new_scene includes BVH build + upload + allocation"}
+            "what": "tray_render, RGBA8 into host memory; new_scene: the first call at this size (BVH build, upload, "
+                    "allocations); new_scene_warm: a new scene once the process has rendered at this size"}
 
 
 def auto_row_step(n_spheres, W, H, spp):
