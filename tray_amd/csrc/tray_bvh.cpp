@@ -72,6 +72,7 @@ constexpr int kSahDepth = 32;
 
 struct Builder {
     std::vector<Prim> prims;
+    std::vector<Prim> scratch;  // split(): the right side while the left is compacted
     std::vector<Node2> bin;
     std::vector<Bvh4Node> nodes;
     std::vector<int32_t> leaves;
@@ -137,40 +138,51 @@ struct Builder {
                 bins[bi].grow(prims[i].box);
                 cnt[bi]++;
             }
+            // Only the occupied bins matter: an empty bin's box grows nothing
+            // (min/max with +-inf are exact) and a split after it has the same
+            // two sides, hence the same cost, as the split after the last
+            // occupied bin before it, which comes first and wins the tie.
+            int occ[kBins], m = 0;
+            for (int i = 0; i < kBins; ++i)
+                if (cnt[i]) occ[m++] = i;
             double right_area[kBins];
             int right_cnt[kBins];
             Box acc;
             int c = 0;
-            for (int i = kBins - 1; i > 0; --i) {
-                acc.grow(bins[i]);
-                c += cnt[i];
-                right_area[i] = acc.area();
-                right_cnt[i] = c;
+            for (int j = m - 1; j > 0; --j) {  // right side of the split before occupied bin j
+                acc.grow(bins[occ[j]]);
+                c += cnt[occ[j]];
+                right_area[j] = acc.area();
+                right_cnt[j] = c;
             }
             Box left;
             int lc = 0;
-            for (int i = 0; i < kBins - 1; ++i) {
-                left.grow(bins[i]);
-                lc += cnt[i];
-                if (lc == 0 || right_cnt[i + 1] == 0) continue;
-                const double cost = left.area() * lc + right_area[i + 1] * right_cnt[i + 1];
+            for (int j = 0; j + 1 < m; ++j) {
+                left.grow(bins[occ[j]]);
+                lc += cnt[occ[j]];
+                const double cost = left.area() * lc + right_area[j + 1] * right_cnt[j + 1];
                 if (cost < best_cost) {
                     best_cost = cost;
                     best_axis = k;
-                    best_bin = i;
+                    best_bin = occ[j];
                 }
             }
         }
         int mid = b;
         if (best_axis >= 0) {
+            // Stable: [b, e) is in list order (see below), so both sides stay in it.
             const int k = best_axis;
             const double ext = cmax[k] - cmin[k];
-            Prim* m = std::partition(prims.data() + b, prims.data() + e, [&](const Prim& p) {
-                int bi = (int)((p.c[k] - cmin[k]) / ext * kBins);
+            scratch.clear();
+            int w = b;
+            for (int i = b; i < e; ++i) {
+                int bi = (int)((prims[i].c[k] - cmin[k]) / ext * kBins);
                 bi = std::min(std::max(bi, 0), kBins - 1);
-                return bi <= best_bin;
-            });
-            mid = (int)(m - prims.data());
+                if (bi <= best_bin) prims[w++] = prims[i];  // w <= i: forward compaction keeps the order
+                else scratch.push_back(prims[i]);
+            }
+            std::copy(scratch.begin(), scratch.end(), prims.begin() + w);
+            mid = w;
         }
         if (mid <= b || mid >= e) {  // median along the widest centroid extent (ties: list order)
             int k = 0;
@@ -180,10 +192,11 @@ struct Builder {
             std::nth_element(prims.begin() + b, prims.begin() + mid, prims.begin() + e, [k](const Prim& x, const Prim& y) {
                 return x.c[k] < y.c[k] || (x.c[k] == y.c[k] && x.index < y.index);
             });
+            // Keep each side's primitives in list order (deterministic, index-ordered leaves).
+            const auto by_index = [](const Prim& x, const Prim& y) { return x.index < y.index; };
+            std::sort(prims.begin() + b, prims.begin() + mid, by_index);
+            std::sort(prims.begin() + mid, prims.begin() + e, by_index);
         }
-        // Keep each side's primitives in list order (deterministic, index-ordered leaves).
-        std::sort(prims.begin() + b, prims.begin() + mid, [](const Prim& x, const Prim& y) { return x.index < y.index; });
-        std::sort(prims.begin() + mid, prims.begin() + e, [](const Prim& x, const Prim& y) { return x.index < y.index; });
         return mid;
     }
 
@@ -286,6 +299,11 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     const int32_t nt = (int32_t)B.prims.size();
     if (nt <= B.leaf_max) return false;  // root must be an inner node
     B.bin.reserve((size_t)2 * nt);
+    B.scratch.reserve((size_t)nt);
+    B.nodes.reserve((size_t)nt);
+    B.leaves.reserve((size_t)nt);
+    B.geo.reserve((size_t)n);
+    B.idx.reserve((size_t)n);
     const int root = B.build2(0, nt, 0);
     B.collapse(root, 0, s);
     std::sort(globals.begin(), globals.end(), [](const Prim& x, const Prim& y) { return x.index < y.index; });
