@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--first-split", action="store_true", help="first time the process renders at this size, piece by piece")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -50,6 +51,21 @@ def main():
         r = f()
         return (time.perf_counter() - t0) * 1e3, r
 
+    if args.first_split:  # the first-at-size costs, piece by piece (a fresh process)
+        t_up, sc0 = ms(lambda: _lib.DeviceScene(fresh(-1), bg))
+
+        def go0():
+            sc0.render_async(cam._state, p, out.data_ptr(), None, stream.cuda_stream)
+            torch.cuda.synchronize()
+        t_l1, _ = ms(go0)
+        t_l2, _ = ms(go0)
+        host = np.empty((H, W, 4), dtype=np.uint8)
+        t_d2h1, _ = ms(lambda: host.__setitem__(slice(None), out.cpu().numpy()))
+        t_d2h2, _ = ms(lambda: host.__setitem__(slice(None), out.cpu().numpy()))
+        sc0.release()
+        print(json.dumps({"first_upload": round(t_up, 3), "first_launch_at_size": round(t_l1, 3),
+                          "second_launch": round(t_l2, 3), "first_d2h_torch": round(t_d2h1, 3),
+                          "second_d2h_torch": round(t_d2h2, 3)}))
     first_at_size, _ = ms(lambda: _lib.render(fresh(-1), bg, cam._state, p))  # bench.py's e2e_ms_new_scene
     rows = {"upload": [], "first_launch": [], "warm_launch": [], "render_new_scene": [], "render_cached": []}
     for k in range(args.reps):

@@ -105,6 +105,23 @@ static int device_state(int32_t device, DeviceState** out) {
         st->checked = true;
         if (!st->usable)
             return fail(TRAY_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+        // The runtime sets up its path for pageable copies of >= 64 KB on their
+        // first use (7-13 ms, tools/hip_h2d_costs.hip); a small first render
+        // never triggers it, so without this the first render of a larger scene
+        // would pay it. Paid here, with the device's other one-time costs.
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        if (hipSetDevice(device) == hipSuccess) {
+            constexpr size_t kWarmBytes = 256 << 10;
+            std::vector<char> h(kWarmBytes, 0);
+            void* d = nullptr;
+            if (hipMalloc(&d, kWarmBytes) == hipSuccess) {
+                (void)hipMemcpy(d, h.data(), kWarmBytes, hipMemcpyHostToDevice);
+                (void)hipMemcpy(h.data(), d, kWarmBytes, hipMemcpyDeviceToHost);
+                (void)hipFree(d);
+            }
+        }
+        (void)hipSetDevice(prev);
     }
     if (!st->usable) return fail(TRAY_ERR_NO_DEVICE, "device is not gfx950");
     *out = st;
