@@ -5,6 +5,15 @@ headline workload (config 2: book-cover scene, seed 2, 1280x720, r=64, d=50).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches its
+own N ranks (one child process per GPU, started before this process touches
+torch or the GPU; RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT
+set per child), waits for all of them and exits non-zero if any fails; rank 0
+prints the JSON line. Under a launcher (WORLD_SIZE set) the ranks are the
+launcher's. Every N > 1 line reports the world RCCL formed and the device
+(PCI bus id, UUID) each rank rendered on; under RCCL the devices must be
+distinct.
+
 A step = one full frame rendered through the C-ABI with the scene already
 resident in HBM; for N > 1 the frame is split into interleaved row tiles
 (default 1 row: rank k renders rows y = k mod N; one shard per rank, no
@@ -103,6 +112,73 @@ def _profile_json(name, config, frames):
     return rec, os.path.relpath(path, ROOT)
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n: int, port: int, base: dict | None = None) -> list:
+    """The environment of each of the n ranks bench.py launches itself (the
+    variables torch.distributed.run would set for --nnodes 1 --nproc-per-node n)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                  "TRAY_BENCH_LAUNCHER": "bench.py"})
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n: int, argv: list, timeout: float | None = None, script: str | None = None) -> int:
+    """Run this script once per rank as child processes (no exec: this process
+    never initialises the GPU) and return 0 only if every rank exits 0. Rank 0's
+    JSON line reaches stdout directly (the children inherit it). When one rank
+    fails the others are stopped (their exact PIDs), so a rank stuck in a
+    collective does not outlive the job."""
+    import subprocess
+
+    cmd = [sys.executable, script or os.path.abspath(__file__)] + list(argv)
+    procs = [subprocess.Popen(cmd, env=e) for e in rank_envs(n, free_port())]
+    rc = 0
+    deadline = None if timeout is None else time.monotonic() + timeout
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        if deadline is not None and time.monotonic() > deadline and live:
+            print(f"bench.py: ranks timed out after {timeout} s", file=sys.stderr)
+            for q in live:
+                q.kill()
+            rc = rc or 124
+            deadline = None
+        time.sleep(0.05)
+    return rc
+
+
+def device_record(torch, local_rank: int) -> dict:
+    """Which device this rank renders on (bench line, `dist.devices`)."""
+    pr = torch.cuda.get_device_properties(local_rank)
+    bus = getattr(pr, "pci_bus_id", None)
+    dom = getattr(pr, "pci_domain_id", 0)
+    dev = getattr(pr, "pci_device_id", 0)
+    return {"device": local_rank, "name": pr.name,
+            "pci": f"{dom:04x}:{bus:02x}:{dev:02x}.0" if bus is not None else None,
+            "uuid": str(getattr(pr, "uuid", "")) or None}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -122,7 +198,14 @@ def main() -> int:
     ap.add_argument("--passes", type=int, default=16,
                     help="frames per launch, the same at every N (tray_render_passes_async: consecutive "
                          "progressive passes in one persistent launch, one tail of long paths per launch)")
+    ap.add_argument("--rank-timeout", type=float, default=None,
+                    help="self-launched ranks (--gpus N > 1 without a launcher): stop them after this many seconds")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # No launcher: start the N ranks here, before anything touches the GPU.
+        return launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout)
 
     import torch
 
@@ -134,10 +217,16 @@ def main() -> int:
     backend = os.environ.get("TRAY_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local_rank = 0
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    if world > 1 and backend == "nccl" and torch.cuda.device_count() < world:
+        print(f"bench.py: --gpus {world} needs {world} visible GPUs, found {torch.cuda.device_count()}",
+              file=sys.stderr)
+        return 2
     torch.cuda.set_device(local_rank)
     dist = None
+    dist_rec = None
     if world > 1:
         import torch.distributed as dist
 
@@ -145,6 +234,15 @@ def main() -> int:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
+        # What the process group saw: its size and every rank's device.
+        devs = [None] * world
+        dist.all_gather_object(devs, dict(device_record(torch, local_rank), rank=rank))
+        keys = [d["pci"] or d["uuid"] or str(d["device"]) for d in devs]
+        if backend == "nccl" and len(set(keys)) != world:
+            print(f"bench.py: RCCL ranks share devices: {keys}", file=sys.stderr)
+            return 3
+        dist_rec = {"backend": backend, "world": dist.get_world_size(), "devices": devs,
+                    "launcher": os.environ.get("TRAY_BENCH_LAUNCHER", "external")}
 
     from tray_amd import _lib, ray, shard
 
@@ -270,6 +368,9 @@ def main() -> int:
         },
         "single_launch_ms": round(single_ms, 4) if single_ms else None,
     }
+    if dist_rec:
+        rec["rccl_world"] = dist_rec["world"] if backend == "nccl" else None
+        rec["dist"] = dist_rec
     if world > 1 and backend != "nccl":
         rec["rehearsal_backend"] = backend  # code-path check only, not a measurement
     if rank == 0:
@@ -387,12 +488,37 @@ def auto_row_step(n_spheres, W, H, spp):
     return max(1, round(W * H * spp * max(n_spheres, 1) / (1280 * 720 * 64 * 486)))
 
 
+def cpu_share() -> tuple:
+    """Threads for the CPU baseline: the CPUs this job may use, not the machine's.
+    BASELINE.md planned w = nproc (GOMAXPROCS, ray/tracer.go:77-79), but on the
+    GPU box nproc reports the whole host while a one-GPU job's share is 16
+    (OMP_NUM_THREADS there); more threads than the share would time the
+    scheduler, not the port. The smallest of the cgroup CPU quota, the affinity
+    mask and OMP_NUM_THREADS, with each figure stated."""
+    seen = {"nproc": os.cpu_count() or 1}
+    try:
+        seen["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            seen["cgroup_quota"] = max(1, int(int(quota) / int(period)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        seen["OMP_NUM_THREADS"] = int(omp)
+    cores = min(seen.values())
+    return cores, "min of " + ", ".join(f"{k}={v}" for k, v in seen.items())
+
+
 def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step):
     """Oracle (C FP64 port of the reference CPU path, chunk-queue scheduler of
     ray/tracer.go:86-116) on every `row_step`-th row of the same frame."""
     from oracle import oracle as O
 
-    cores = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+    cores, why = cpu_share()
     rows = np.arange(0, H, row_step, dtype=np.int32)
     bg = np.array([1.0, 1.0, 1.0, 0.4, 0.65, 1.0])
     t0 = time.perf_counter()
@@ -400,7 +526,7 @@ def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step):
     dt = time.perf_counter() - t0
     samples = len(rows) * W * spp
     return {"value": round(samples / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "seconds": round(dt, 3), "cpu_model": cpu_model(),
+            "seconds": round(dt, 3), "cpu_model": cpu_model(), "cores_reason": why,
             "sample": f"every {row_step}. row of the same frame ({len(rows)} rows x {W} px x r={spp}), "
                       f"oracle/tray_oracle.c, {cores} pthreads"}
 

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define TRAY_ABI_VERSION 1
+#define TRAY_ABI_VERSION 2 /* 2: tray_render_devices_progress, tray_release_cache */
 
 typedef enum tray_status {
     TRAY_OK = 0,
@@ -166,6 +166,17 @@ const char *tray_last_error(void);
 int tray_device_count(int32_t *count);
 /* Free every library-owned device buffer on every device. */
 int tray_shutdown(void);
+/* Free what the synchronous entry points (tray_render, tray_render_progress,
+ * tray_render_devices*) keep on `device` (every device when device < 0): per
+ * render slot, the last uploaded scene with its sample buffer (24 B per sample
+ * of a launch band: up to ~25.8 GB at 2^30 samples, e.g. a 3840x2160 r=1024
+ * band) and candidate records, the output workspaces, the stream and the
+ * progress counters. A device listed k times in one tray_render_devices call
+ * keeps k slots. Long-lived callers that share the device with other users call
+ * this between renders; the next synchronous render re-uploads. Scenes from
+ * tray_scene_upload are the caller's and are not touched. No reference
+ * counterpart (Go's Render allocates per call, ray/tracer.go:38-45). */
+int tray_release_cache(int32_t device);
 
 /* ---- host-side setup (ray/camera.go, ray/objects.go) ------------------------ */
 /* Camera.Initialize (ray/camera.go:43-105): applies zero-field defaults to
@@ -198,16 +209,22 @@ int tray_render(const tray_sphere *spheres, int32_t n_spheres, const tray_backgr
 /* Live progress of a synchronous render (Tracer.ProgressFunc, called per row
  * while rendering, ray/tracer.go:126-128): `rows` more rows of the row set have
  * all their samples finished. Called on the thread that called
- * tray_render_progress, before it returns; the rows sum to the row count. */
+ * tray_render_progress / tray_render_devices_progress, before it returns; the
+ * rows sum to the row count.
+ * The callback runs while the render holds its devices: it must not call back
+ * into this library's synchronous entry points (tray_render*, tray_shutdown,
+ * tray_release_cache, tray_linear_to_srgba_async), which then fail with
+ * TRAY_ERR_INVALID_ARGUMENT instead of deadlocking. Keep it short (a Go
+ * callback should only bump a counter, as ray/tracer_test.go:174-176 does). */
 typedef void (*tray_progress_fn)(int32_t rows, void *user);
 
 /* tray_render with live progress: the device counts finished samples per 8-row
  * tile row and the calling thread polls the counters (every ~0.5 ms) while the
  * launch runs, calling progress(rows, user) as tile rows complete. progress may
  * be NULL (then this is tray_render). The synchronous entry points keep the
- * last scene they uploaded on each device and reuse it while the caller passes
- * identical spheres and background (compared byte for byte); tray_shutdown()
- * releases it. */
+ * last scene they uploaded on each device (with its sample buffer) and reuse it
+ * while the caller passes identical spheres and background (compared byte for
+ * byte); tray_release_cache(device) or tray_shutdown() releases it. */
 int tray_render_progress(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
                          const tray_camera *camera, const tray_params *params, int32_t device, void *out,
                          uint32_t *segments_out, tray_progress_fn progress, void *user);
@@ -223,6 +240,16 @@ int tray_render_progress(const tray_sphere *spheres, int32_t n_spheres, const tr
 int tray_render_devices(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
                         const tray_camera *camera, const tray_params *params, const int32_t *devices,
                         int32_t n_devices, void *out, uint32_t *segments_out);
+
+/* tray_render_devices with live progress: every device counts its shard's
+ * finished samples per 8-row tile row, and the calling thread polls all of them
+ * while the devices render, calling progress(rows, user) as tile rows complete on
+ * any device (ProgressFunc from any worker, ray/tracer.go:126-128). progress may
+ * be NULL (then this is tray_render_devices). */
+int tray_render_devices_progress(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
+                                 const tray_camera *camera, const tray_params *params, const int32_t *devices,
+                                 int32_t n_devices, void *out, uint32_t *segments_out, tray_progress_fn progress,
+                                 void *user);
 
 /* Device-resident scene for repeated renders (the scene is read-only during
  * Render, ray/tracer.go:48). */

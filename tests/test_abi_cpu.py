@@ -19,7 +19,7 @@ def test_exports_match_header(L):
     lib = L.lib()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.tray_abi_version() == 1
+    assert lib.tray_abi_version() == 2  # 2: tray_render_devices_progress, tray_release_cache
 
 
 def _setup(L, arr):
@@ -250,3 +250,27 @@ def test_render_devices_argument_checks(L):
     if not os.path.exists("/dev/kfd"):
         assert lib.tray_render_devices(None, 0, ctypes.byref(bg), ctypes.byref(cam), ctypes.byref(p), devs, 2,
                                        out.ctypes.data, None) == L.TRAY_ERR_NO_DEVICE
+
+
+def test_import_order_library_before_torch():
+    """`import tray_amd` (and loading the library) BEFORE torch: both link a
+    libamdhip64.so.7, and torch only works on its own bundled copy. The binding
+    loads torch first, so one HIP runtime is mapped and it is torch's."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from tray_amd import _lib, ray\n"
+        "_lib.lib(); ray.DefaultBackground()\n"
+        "import torch\n"
+        "torch.cuda.device_count()\n"
+        "maps = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+        "print(len(maps), sorted(maps)[0])\n" % ROOT
+    )
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    n, path = r.stdout.split()
+    import torch
+
+    assert n == "1" and os.path.realpath(path).startswith(os.path.realpath(os.path.dirname(torch.__file__))), path

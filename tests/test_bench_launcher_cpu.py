@@ -1,0 +1,93 @@
+"""bench.py's own N-rank launcher (`--gpus N` with no WORLD_SIZE): the rank
+environments, the child-process supervision and the refusal paths, on CPU.
+
+The reference's parallelism lives inside one Render call (NumWorkers
+goroutines, ray/tracer.go:86-116); bench.py's N-GPU line must come out of
+`python bench.py --gpus N` alone, one process per GPU."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_rank_envs_match_torchrun_single_node():
+    envs = bench.rank_envs(4, 29555, base={"PATH": "/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    for e in envs:
+        assert e["WORLD_SIZE"] == "4" and e["LOCAL_WORLD_SIZE"] == "4"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29555"
+        assert e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["PATH"] == "/bin"  # inherited
+        assert e["TRAY_BENCH_LAUNCHER"] == "bench.py"
+
+
+def test_free_port_is_bindable():
+    import socket
+
+    p = bench.free_port()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", p))
+
+
+def _script(tmp_path, body):
+    path = tmp_path / "rank.py"
+    path.write_text("import os, sys, time\n" + body)
+    return str(path)
+
+
+def test_launch_ranks_runs_every_rank(tmp_path):
+    out = tmp_path / "out"
+    out.mkdir()
+    script = _script(tmp_path, f"open(os.path.join({str(out)!r}, os.environ['RANK']), 'w').write("
+                               "os.environ['WORLD_SIZE'] + ' ' + os.environ['MASTER_PORT'] + ' ' + ' '.join(sys.argv[1:]))\n")
+    assert bench.launch_ranks(3, ["--steps", "7"], timeout=60, script=script) == 0
+    got = sorted(os.listdir(out))
+    assert got == ["0", "1", "2"]
+    lines = {(out / r).read_text() for r in got}
+    assert len(lines) == 1  # one port, one world, the same arguments for every rank
+    world, port, *argv = lines.pop().split()
+    assert world == "3" and int(port) > 0 and argv == ["--steps", "7"]
+
+
+def test_launch_ranks_fails_and_stops_the_others(tmp_path):
+    # rank 1 fails at once; rank 0 would sleep for a minute (a rank stuck in a collective)
+    script = _script(tmp_path, "if os.environ['RANK'] == '1': sys.exit(5)\ntime.sleep(60)\n")
+    t0 = __import__("time").monotonic()
+    assert bench.launch_ranks(2, [], timeout=120, script=script) == 5
+    assert __import__("time").monotonic() - t0 < 30
+
+
+def test_launch_ranks_timeout(tmp_path):
+    script = _script(tmp_path, "time.sleep(60)\n")
+    assert bench.launch_ranks(2, [], timeout=1.0, script=script) == 124
+
+
+def test_cpu_share_states_its_reason():
+    cores, why = bench.cpu_share()
+    assert 1 <= cores <= (os.cpu_count() or 1)
+    assert "nproc=" in why
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="checks the no-GPU refusal")
+def test_self_launch_without_gpus_fails_loudly():
+    """`bench.py --gpus 2` with no launcher starts two ranks; without GPUs each
+    refuses (RCCL needs one device per rank) and the parent exits non-zero."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TRAY_BENCH_BACKEND")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rank-timeout", "240"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0
+    assert "needs 2 visible GPUs" in r.stderr
+    assert r.stdout.strip() == ""  # no JSON line from a failed job
+
+
+def test_world_mismatch_is_refused():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, env=env, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in r.stderr

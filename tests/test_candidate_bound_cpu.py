@@ -32,7 +32,7 @@ def beam(cam, spp, ray_radius, xa, xb, ya, yb):
     s0 = p00 + pxv * (0.5 * (xa + xb)) + pyv * (0.5 * (ya + yb))
     b0 = pos + (s0 - pos) * ft if lens else s0
     lx, ly = np.linalg.norm(pxv), np.linalg.norm(pyv)
-    aa = (ray_radius * np.hypot(lx, ly) if spp > 1 else 0.0) + 0.5 * (xb - xa) * lx + 0.5 * (yb - ya) * ly
+    aa = (abs(ray_radius) * np.hypot(lx, ly) if spp > 1 else 0.0) + 0.5 * (xb - xa) * lx + 0.5 * (yb - ya) * ly
     ra = np.sqrt(du @ du + dv @ dv) if lens else 0.0
     rb = aa * abs(ft) if lens else aa
     return pos, b0 - pos, ra, rb
@@ -107,6 +107,8 @@ CAMS = {
     "rich_dof": (RICH_SETUP, 64, 0.5),
     "rich_pinhole_r1": (np.r_[RICH_SETUP[:12], 0.0], 1, 0.5),
     "rich_big_aperture_radius2": (np.r_[RICH_SETUP[:12], 1.5], 16, 2.0),
+    # Go accepts a negative RayRadius (InDisc(r) scales by the signed r): the disc's extent is |r|
+    "rich_negative_radius": (RICH_SETUP, 16, -1.5),
     "top_down": (np.array([0.5, 15, 0.2, 0, 0, 0, 0, 0, 1, 60.0, 1.0, 15.0, 0.3]), 4, 0.5),
 }
 

@@ -66,6 +66,7 @@ CASES = {
     "book_pinhole_r4": ("rich2", np.r_[RICH_SETUP[:12], 0.0], 120, 68, 4, 20, 0.5, 4, {}),
     "book_dof_r1": ("rich2", RICH_SETUP, 120, 68, 1, 20, 0.5, 6, {}),
     "book_radius2": ("rich2", RICH_SETUP, 96, 54, 4, 20, 2.0, 11, {}),
+    "book_negative_radius": ("rich2", RICH_SETUP, 96, 54, 16, 20, -2.0, 13, {}),
     "book_wide_fov": ("rich2", np.r_[RICH_SETUP[:9], 120.0, RICH_SETUP[10:]], 128, 72, 4, 20, 0.5, 12, {}),
     "book_narrow_fov": ("rich2", np.r_[RICH_SETUP[:9], 4.0, RICH_SETUP[10:]], 128, 72, 4, 20, 0.5, 13, {}),
     "book_top_down": ("rich2", np.array([0.5, 15, 0.2, 0, 0, 0, 0, 0, 1, 60.0, 1.0, 15.0, 0.3]), 96, 96, 4, 20,
@@ -155,7 +156,7 @@ def test_candidate_cache_follows_camera_and_rows(L, O):
 
 def test_candidates_equal_traversal_random_cameras(L, O):
     """24 random cameras (position inside and outside the spheres, any target,
-    field of view 5-150 degrees, aperture 0-3, focus 0.5-30, AA radius 0-3) on the
+    field of view 5-150 degrees, aperture 0-3, focus 0.5-30, AA radius -3..3: Go takes a signed RayRadius) on the
     adversarial scene and the dense scene: identical frames with and without
     candidate lists."""
     rng = np.random.default_rng(2024)
@@ -172,7 +173,7 @@ def test_candidates_equal_traversal_random_cameras(L, O):
         focus = rng.uniform(0.5, 30)
         setup = np.r_[frm, at, [0, 1, 0], vfov, 1.0, focus, aperture]
         spp = [1, 2, 4][k % 3]
-        radius = rng.uniform(0, 3)
+        radius = rng.uniform(-3, 3)
         (rgb, seg), (ref, rseg) = both(L, sc, setup, 48, 32, spp, 8, radius, 100 + k)
         assert np.array_equal(seg, rseg), (k, setup, spp, radius)
         assert np.array_equal(rgb, ref, equal_nan=True), (k, setup, spp, radius)

@@ -67,6 +67,9 @@ CASES = {
     "book_r1_pinhole": ("rich2", np.r_[RICH_SETUP[:12], 0.0], 80, 45, 1, 50, 0.5, 3),
     "book_radius1": ("rich2", RICH_SETUP, 40, 30, 6, 20, 1.0, 11),
     "book_depth1": ("rich2", RICH_SETUP, 40, 30, 3, 1, 0.5, 4),
+    # Go's RenderLines takes a negative RayRadius (InDisc scales by the signed r): the candidate
+    # lists must bound the disc by |r|
+    "book_negative_radius": ("rich2", RICH_SETUP, 64, 36, 8, 50, -1.5, 12),
     "dense_seed7": ("dense7", RICH_SETUP, 48, 27, 2, 50, 0.5, 7),
     "empty": ("empty", RICH_SETUP, 33, 17, 4, 50, 0.5, 5),
     "seed_zero_and_big": ("rich2", RICH_SETUP, 21, 13, 5, 50, 0.5, 0),

@@ -113,10 +113,14 @@ def test_render_to_png(ray, tmp_path):  # benchmark/benchmark.go:23-33: png.Enco
     assert np.array_equal(png.decode_png(open(path, "rb").read()), img)
 
 
-def test_progress_is_live(ray):  # tracer.go:126-128: ProgressFunc per row WHILE rendering
-    """tray_render_progress reports rows as their samples finish, from device
-    counters polled during the launch: several callbacks, the first well before
-    the end, every row exactly once; Tracer.ProgressFunc sees width per row."""
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_progress_is_live(ray, devices):  # tracer.go:126-128: ProgressFunc per row WHILE rendering
+    """tray_render_progress (one device) and tray_render_devices_progress (the
+    rows split over several devices of the process; device 0 twice here) report
+    rows as their samples finish, from device counters polled during the
+    launches: several callbacks, the first well before the end, every row exactly
+    once, and the same frame as without progress; Tracer.ProgressFunc sees width
+    per row."""
     import time
 
     from tray_amd import _lib
@@ -127,21 +131,76 @@ def test_progress_is_live(ray):  # tracer.go:126-128: ProgressFunc per row WHILE
     spheres = ray.rich_scene_array(2)
     bg = ray._background(ray.DefaultBackground())
     p = _lib.make_params(W, H, 50, 256, 0.5, 2, output=_lib.OUT_RGB_F32)
-    _lib.render(spheres, bg, cam._state, p)  # warm: scene upload + sample buffer
+
+    def render(**kw):
+        if len(devices) == 1:
+            return _lib.render(spheres, bg, cam._state, p, devices[0], **kw)[0]
+        return _lib.render_devices(spheres, bg, cam._state, p, devices, **kw)[0]
+
+    plain = render()  # also warms: scene upload + sample buffer
     calls = []
     t0 = time.perf_counter()
-    _lib.render(spheres, bg, cam._state, p, progress=lambda rows: calls.append((time.perf_counter(), rows)))
+    live = render(progress=lambda rows: calls.append((time.perf_counter(), rows)))
     t1 = time.perf_counter()
+    assert np.array_equal(plain, live)
     assert sum(r for _, r in calls) == H
     assert len(calls) >= 3, calls
     assert calls[0][1] < H and calls[0][0] < t0 + 0.8 * (t1 - t0)
     t = ray.New(64, 36)
     t.Camera = ray.RichSceneCamera()
     t.NumRaysPerPixel, t.MaxDepth, t.Seed = 16, 20, 2
+    t.Devices = devices
     seen = []
     t.ProgressFunc = seen.append
     t.Render(ray.RichScene(2))
     assert seen == [64] * 36
+
+
+def test_progress_callback_errors_and_reentry(ray):
+    """A ProgressFunc that raises: the render finishes and the exception reaches
+    the caller (ctypes would swallow it). A callback that calls back into the
+    library gets an error instead of a deadlock (the render holds the device)."""
+    from tray_amd import _lib
+
+    t = ray.New(64, 36)
+    t.Camera = ray.RichSceneCamera()
+    t.NumRaysPerPixel, t.MaxDepth, t.Seed = 4, 20, 2
+
+    def boom(_w):
+        raise KeyError("from ProgressFunc")
+
+    t.ProgressFunc = boom
+    with pytest.raises(KeyError, match="from ProgressFunc"):
+        t.Render(ray.RichScene(2))
+    codes = []
+
+    def reenter(_rows):
+        codes.append(_lib.lib().tray_release_cache(0))
+        codes.append(_lib.lib().tray_shutdown())
+
+    cam = ray.RichSceneCamera()
+    cam.Initialize(32, 18)
+    p = _lib.make_params(32, 18, 10, 2, 0.5, 2)
+    _lib.render(ray.rich_scene_array(2), ray._background(ray.DefaultBackground()), cam._state, p, progress=reenter)
+    assert codes and all(c == _lib.TRAY_ERR_INVALID_ARGUMENT for c in codes)
+    assert "not re-entrant" in _lib.lib().tray_last_error().decode()
+
+
+def test_release_cache(ray):
+    """tray_release_cache frees the synchronous renders' cached scene and
+    buffers; the next render re-uploads and gives the same frame."""
+    from tray_amd import _lib
+
+    cam = ray.RichSceneCamera()
+    cam.Initialize(48, 27)
+    p = _lib.make_params(48, 27, 20, 4, 0.5, 2)
+    args = (ray.rich_scene_array(2), ray._background(ray.DefaultBackground()), cam._state, p)
+    a, _ = _lib.render(*args)
+    _lib.release_cache(0)
+    b, _ = _lib.render(*args)
+    _lib.release_cache(-1)
+    c, _ = _lib.render_devices(*args, [0, 0])
+    assert np.array_equal(a, b) and np.array_equal(a, c)
 
 
 def test_tracer_devices_split_is_invisible(ray):

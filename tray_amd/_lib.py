@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -129,6 +130,8 @@ EXPORTS = (
     "tray_render",
     "tray_render_progress",
     "tray_render_devices",
+    "tray_render_devices_progress",
+    "tray_release_cache",
     "tray_scene_upload",
     "tray_scene_release",
     "tray_scene_get_info",
@@ -146,6 +149,20 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_void_p)
 _libs: dict = {}
 
 
+def _torch_first() -> None:
+    """Load torch (when it is installed) before the library. Both link a HIP
+    runtime with the same soname (libamdhip64.so.7): torch bundles its own, the
+    library was linked against /opt/rocm's. Whichever is mapped first serves
+    both, and torch does not work on /opt/rocm's (it then sees no GPU), while
+    the library's C-ABI works on either. Importing torch here makes the import
+    order of `tray_amd` and `torch` irrelevant to the caller."""
+    import importlib.util
+
+    if "torch" in sys.modules or importlib.util.find_spec("torch") is None:
+        return
+    import torch  # noqa: F401
+
+
 def lib(path: str | None = None) -> ctypes.CDLL:
     """The C-ABI library (default: the in-tree build). `path` loads another build
     of the same ABI (used by tools/ab_bench.py to compare kernel variants)."""
@@ -157,6 +174,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
             f"{path} is missing: the HIP renderer is not built. Run `make -C tray_amd` "
             "(or __graft_entry__.build()). There is no CPU fallback."
         )
+    _torch_first()
     L = ctypes.CDLL(path)
     vp, i32, u32p = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32)
     L.tray_abi_version.restype = i32
@@ -176,6 +194,10 @@ def lib(path: str | None = None) -> ctypes.CDLL:
     if hasattr(L, "tray_render_devices"):
         L.tray_render_devices.argtypes = [vp, i32, ctypes.POINTER(Background), ctypes.POINTER(CameraState),
                                           ctypes.POINTER(Params), ctypes.POINTER(i32), i32, vp, u32p]
+    if hasattr(L, "tray_render_devices_progress"):
+        L.tray_render_devices_progress.argtypes = L.tray_render_devices.argtypes + [PROGRESS_FN, vp]
+    if hasattr(L, "tray_release_cache"):
+        L.tray_release_cache.argtypes = [i32]
     if hasattr(L, "tray_linear_to_srgba_async"):
         L.tray_linear_to_srgba_async.argtypes = [vp, ctypes.c_size_t, vp, i32, vp]
     L.tray_scene_upload.argtypes = [vp, i32, ctypes.POINTER(Background), i32, ctypes.POINTER(vp)]
@@ -240,15 +262,42 @@ def render(spheres, background: Background, camera: CameraState, params: Params,
     if progress is None:
         check(lib().tray_render(*args))
     else:
-        cb = PROGRESS_FN(lambda rows, _user: progress(int(rows)))  # kept alive for the call
-        check(lib().tray_render_progress(*args, cb, None))
+        with _Progress(progress) as cb:
+            check(lib().tray_render_progress(*args, cb.fn, None))
     return out, seg
 
 
+class _Progress:
+    """A Python progress callback behind tray_progress_fn. ctypes swallows an
+    exception raised inside a callback; this keeps the first one, stops calling
+    the function after it, and re-raises it when the render returns."""
+
+    def __init__(self, fn):
+        self.user, self.error = fn, None
+        self.fn = PROGRESS_FN(self._call)  # kept alive for the call
+
+    def _call(self, rows, _user):
+        if self.error is not None:
+            return
+        try:
+            self.user(int(rows))
+        except BaseException as e:  # noqa: BLE001 - re-raised after the render
+            self.error = e
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if et is None and self.error is not None:
+            raise self.error
+        return False
+
+
 def render_devices(spheres, background: Background, camera: CameraState, params: Params, devices,
-                   segments: bool = False):
+                   segments: bool = False, progress=None):
     """tray_render_devices: the row set split over `devices` (interleaved 1-row
-    tiles, a device may repeat), rows returned in image order like render()."""
+    tiles, a device may repeat), rows returned in image order like render().
+    progress(rows): tray_render_devices_progress, called as rows finish on any device."""
     s = spheres_array(spheres)
     rows = params_rows(params)
     ch = 4 if params.output == OUT_RGBA8 else 3
@@ -256,10 +305,20 @@ def render_devices(spheres, background: Background, camera: CameraState, params:
     out = np.zeros((rows, params.width, ch), dtype=dtype)
     seg = np.zeros((rows, params.width), dtype=np.uint32) if segments else None
     devs = (ctypes.c_int32 * len(devices))(*devices)
-    check(lib().tray_render_devices(s.ctypes.data if len(s) else None, len(s), ctypes.byref(background),
-                                    ctypes.byref(camera), ctypes.byref(params), devs, len(devices), out.ctypes.data,
-                                    seg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) if seg is not None else None))
+    args = (s.ctypes.data if len(s) else None, len(s), ctypes.byref(background), ctypes.byref(camera),
+            ctypes.byref(params), devs, len(devices), out.ctypes.data,
+            seg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) if seg is not None else None)
+    if progress is None:
+        check(lib().tray_render_devices(*args))
+    else:
+        with _Progress(progress) as cb:
+            check(lib().tray_render_devices_progress(*args, cb.fn, None))
     return out, seg
+
+
+def release_cache(device: int = -1) -> None:
+    """tray_release_cache: free what the synchronous renders keep on `device` (all: -1)."""
+    check(lib().tray_release_cache(int(device)))
 
 
 def linear_to_srgba_async(rgb_ptr: int, n_pixels: int, rgba_ptr: int, device: int = 0, stream: int | None = None):

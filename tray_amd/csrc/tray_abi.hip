@@ -56,19 +56,22 @@ struct Slot {
     tray_scene_s* cached = nullptr;
     std::vector<tray_sphere> cached_spheres;
     tray_background cached_bg;
+    // Live progress: samples finished per 8-row tile row of the slot's compact
+    // rows, in host-mapped coherent memory the kernel adds to (system-scope
+    // atomics) and the calling thread polls.
+    unsigned long long* prog_host = nullptr;
+    unsigned long long* prog_dev = nullptr;  // its device address
+    size_t prog_bytes = 0;
 };
 
-// Per-device state: render slots, the progress counters and the sRGB encoder
-// table of tray_linear_to_srgba_async.
+// Per-device state: render slots and the sRGB encoder table of
+// tray_linear_to_srgba_async.
 struct DeviceState {
     std::mutex mu;
     bool checked = false;
     bool usable = false;
     std::deque<Slot> slots;  // a deque: growing it keeps references to existing slots valid
-    uint32_t* prog_host = nullptr;  // samples finished per 8-row tile row (host-mapped, coherent)
-    uint32_t* prog_dev = nullptr;   // its device address
-    size_t prog_bytes = 0;
-    double* srgb = nullptr;         // tray::srgb_thresholds on the device
+    double* srgb = nullptr;  // tray::srgb_thresholds on the device
     Slot& slot(size_t j) {
         if (slots.size() <= j) slots.resize(j + 1);
         return slots[j];
@@ -77,6 +80,16 @@ struct DeviceState {
 
 static std::mutex g_devices_mu;
 static std::vector<DeviceState*> g_devices;
+
+// Set while a progress callback runs on this thread: the entry points that
+// take a device's lock refuse to run from inside one (the render that called
+// back still holds that lock), instead of deadlocking.
+thread_local bool g_in_progress_callback = false;
+
+static int refuse_reentry(const char* fn) {
+    return fail(TRAY_ERR_INVALID_ARGUMENT,
+                std::string(fn) + " called from a tray_progress_fn: the library is not re-entrant from its callbacks");
+}
 
 static int visible_devices(int* count) {
     int n = 0;
@@ -433,7 +446,7 @@ static bool cand_enabled() {
 
 static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
                              uint32_t* segments_device, unsigned long long* stats_device, void* stream,
-                             int32_t n_passes = 1, uint32_t* progress_device = nullptr) {
+                             int32_t n_passes = 1, unsigned long long* progress_device = nullptr) {
     if (!sc || !cam || !out_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     int rc = validate_params(p);
     if (rc) return rc;
@@ -623,6 +636,80 @@ static hipError_t prepare_slot(Slot& sl, size_t out_bytes, size_t seg_bytes) {
     return e;
 }
 
+// The slot's progress counters for `rows` compact rows (one per 8-row tile row),
+// zeroed. The slot's stream is idle here (synchronous entry points only).
+static hipError_t prepare_progress(Slot& sl, int32_t rows) {
+    const size_t bytes = (size_t)((rows + 7) / 8) * sizeof(unsigned long long);
+    if (sl.prog_bytes < bytes) {
+        if (sl.prog_host) (void)hipHostFree(sl.prog_host);
+        sl.prog_host = nullptr;
+        sl.prog_dev = nullptr;
+        sl.prog_bytes = 0;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&sl.prog_host), bytes,
+                                     hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&sl.prog_dev), sl.prog_host, 0);
+        if (e != hipSuccess) return e;
+        sl.prog_bytes = bytes;
+    }
+    memset(sl.prog_host, 0, bytes);
+    return hipSuccess;
+}
+
+// One rendering shard whose progress counters the calling thread polls.
+struct ProgressWatch {
+    int device;
+    Slot* slot;
+    int32_t rows;        // compact rows of the shard
+    uint64_t per_row;    // samples of one row: width x rays_per_pixel
+    std::vector<uint8_t> done;  // per tile row: reported
+};
+
+// Poll every watched shard's counters until all their streams are idle, and
+// report the rows of each tile row whose samples have all finished
+// (ProgressFunc, ray/tracer.go:126-128: per row, while rendering). A
+// device-to-host copy could not be used: it would queue behind the persistent
+// grid that holds every CU. Returns the rows reported; `e` gets a stream error.
+static int32_t poll_progress(std::vector<ProgressWatch>& ws, tray_progress_fn progress, void* user, hipError_t& e) {
+    int32_t reported = 0;
+    for (ProgressWatch& w : ws) w.done.assign((size_t)((w.rows + 7) / 8), 0);
+    while (true) {
+        bool busy = false;
+        for (ProgressWatch& w : ws) {
+            (void)hipSetDevice(w.device);
+            const hipError_t q = hipStreamQuery(w.slot->stream);
+            if (q == hipErrorNotReady) busy = true;
+            else if (q != hipSuccess && e == hipSuccess) e = q;
+        }
+        if (!busy || e != hipSuccess) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(500));
+        int32_t fresh = 0;
+        for (ProgressWatch& w : ws) {
+            const volatile unsigned long long* counts = w.slot->prog_host;
+            for (size_t t = 0; t < w.done.size(); ++t) {
+                const int32_t r = std::min(8, w.rows - 8 * (int32_t)t);
+                if (!w.done[t] && (uint64_t)counts[t] >= (uint64_t)r * w.per_row) {
+                    w.done[t] = 1;
+                    fresh += r;
+                }
+            }
+        }
+        if (fresh) {
+            g_in_progress_callback = true;
+            progress(fresh, user);
+            g_in_progress_callback = false;
+            reported += fresh;
+        }
+    }
+    return reported;
+}
+
+static void report_rest(tray_progress_fn progress, void* user, int32_t rows, int32_t reported) {
+    if (!progress || reported >= rows) return;
+    g_in_progress_callback = true;
+    progress(rows - reported, user);
+    g_in_progress_callback = false;
+}
+
 int tray_render(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,
                 const tray_params* p, int32_t device, void* out, uint32_t* segments_out) {
     return tray_render_progress(spheres, n, bg, cam, p, device, out, segments_out, nullptr, nullptr);
@@ -631,6 +718,7 @@ int tray_render(const tray_sphere* spheres, int32_t n, const tray_background* bg
 int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,
                          const tray_params* p, int32_t device, void* out, uint32_t* segments_out,
                          tray_progress_fn progress, void* user) {
+    if (g_in_progress_callback) return refuse_reentry("tray_render");
     if (!bg || !cam || !out) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     int rc = validate_params(p);
     if (rc) return rc;
@@ -652,51 +740,19 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
     const size_t out_bytes = npix * bytes_per_pixel(p->output);
     const size_t seg_bytes = npix * sizeof(uint32_t);
     e = prepare_slot(sl, out_bytes, segments_out ? seg_bytes : 0);
-    // Progress: one counter of finished samples per 8-row tile row of the compact rows.
-    const int32_t tile_rows = (rows + 7) / 8;
-    const size_t prog_bytes = (size_t)tile_rows * sizeof(uint32_t);
-    if (e == hipSuccess && progress && st->prog_bytes < prog_bytes) {
-        // counters in host memory the kernel adds to (system-scope atomics) and this
-        // thread reads: a device-to-host copy would queue behind the persistent grid
-        if (st->prog_host) (void)hipHostFree(st->prog_host);
-        st->prog_host = nullptr;
-        st->prog_dev = nullptr;
-        st->prog_bytes = 0;
-        e = hipHostMalloc(&st->prog_host, prog_bytes, hipHostMallocMapped | hipHostMallocCoherent);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&st->prog_dev), st->prog_host, 0);
-        if (e == hipSuccess) st->prog_bytes = prog_bytes;
-    }
-    if (e == hipSuccess && progress) memset(st->prog_host, 0, prog_bytes);  // the stream is idle here
+    if (e == hipSuccess && progress) e = prepare_progress(sl, rows);
     if (e != hipSuccess) return hip_fail(e, "workspace");
     rc = render_async_impl(sc, cam, p, sl.out_ws, segments_out ? sl.seg_ws : nullptr, nullptr, sl.stream, 1,
-                           progress ? st->prog_dev : nullptr);
+                           progress ? sl.prog_dev : nullptr);
     if (rc) {  // a band may already be enqueued: let it finish before the slot can be reused
         (void)hipStreamSynchronize(sl.stream);
         return rc;
     }
-    // Poll the counters while the launch runs and report the rows of every tile
-    // row whose samples have all finished (ProgressFunc, ray/tracer.go:126-128).
     // Before the copies: a copy into pageable caller memory returns only once done.
     int32_t reported = 0;
     if (progress) {
-        const uint64_t per_row = (uint64_t)p->width * (uint64_t)p->rays_per_pixel;
-        std::vector<uint8_t> done((size_t)tile_rows, 0);
-        const volatile uint32_t* counts = st->prog_host;
-        while ((e = hipStreamQuery(sl.stream)) == hipErrorNotReady) {
-            std::this_thread::sleep_for(std::chrono::microseconds(500));
-            int32_t fresh = 0;
-            for (int32_t t = 0; t < tile_rows; ++t) {
-                const int32_t r = std::min(8, rows - 8 * t);
-                if (!done[(size_t)t] && (uint64_t)counts[t] >= (uint64_t)r * per_row) {
-                    done[(size_t)t] = 1;
-                    fresh += r;
-                }
-            }
-            if (fresh) {
-                progress(fresh, user);
-                reported += fresh;
-            }
-        }
+        std::vector<ProgressWatch> ws{ProgressWatch{device, &sl, rows, (uint64_t)p->width * (uint64_t)p->rays_per_pixel, {}}};
+        reported = poll_progress(ws, progress, user, e);
         if (e != hipSuccess) return hip_fail(e, "render");
     }
     e = hipMemcpyAsync(out, sl.out_ws, out_bytes, hipMemcpyDeviceToHost, sl.stream);
@@ -704,13 +760,22 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
         e = hipMemcpyAsync(segments_out, sl.seg_ws, seg_bytes, hipMemcpyDeviceToHost, sl.stream);
     if (e == hipSuccess) e = hipStreamSynchronize(sl.stream);
     if (e != hipSuccess) return hip_fail(e, "render");
-    if (progress && reported < rows) progress(rows - reported, user);
+    report_rest(progress, user, rows, reported);
     return TRAY_OK;
 }
 
 int tray_render_devices(const tray_sphere* spheres, int32_t n, const tray_background* bg, const tray_camera* cam,
                         const tray_params* p, const int32_t* devices, int32_t n_devices, void* out,
                         uint32_t* segments_out) {
+    return tray_render_devices_progress(spheres, n, bg, cam, p, devices, n_devices, out, segments_out, nullptr,
+                                        nullptr);
+}
+
+int tray_render_devices_progress(const tray_sphere* spheres, int32_t n, const tray_background* bg,
+                                 const tray_camera* cam, const tray_params* p, const int32_t* devices,
+                                 int32_t n_devices, void* out, uint32_t* segments_out, tray_progress_fn progress,
+                                 void* user) {
+    if (g_in_progress_callback) return refuse_reentry("tray_render_devices");
     if (!bg || !cam || !out || !devices) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     if (n_devices < 1 || n_devices > 1024) return fail(TRAY_ERR_INVALID_ARGUMENT, "n_devices must be in [1, 1024]");
     int rc = validate_params(p);
@@ -744,6 +809,13 @@ int tray_render_devices(const tray_sphere* spheres, int32_t n, const tray_backgr
     hipError_t e = hipSuccess;
     // Shard k renders the interleaved 1-row tiles k, k + n, ... of the row set
     // (tile k -> shard k mod n), each on its own slot and stream.
+    auto drain = [&](int32_t upto) {  // let what is enqueued finish before the slots can be reused
+        for (int32_t j = 0; j < upto; ++j)
+            if (shards[(size_t)j].rows > 0 && shards[(size_t)j].slot->stream) {
+                (void)hipSetDevice(shards[(size_t)j].device);
+                (void)hipStreamSynchronize(shards[(size_t)j].slot->stream);
+            }
+    };
     for (int32_t k = 0; k < n_devices; ++k) {
         const size_t u = (size_t)(std::lower_bound(uniq.begin(), uniq.end(), devices[k]) - uniq.begin());
         Shard& sh = shards[(size_t)k];
@@ -756,25 +828,42 @@ int tray_render_devices(const tray_sphere* spheres, int32_t n, const tray_backgr
         sh.rows = tray_params_rows(&sh.params);
         if (sh.rows == 0) continue;
         e = hipSetDevice(sh.device);
-        if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+        if (e != hipSuccess) {
+            drain(k);
+            return hip_fail(e, "hipSetDevice");
+        }
         tray_scene_t sc = nullptr;
         rc = cached_scene(*sh.slot, spheres, n, bg, sh.device, &sc);
-        if (rc) return rc;
+        if (rc) {
+            drain(k);
+            return rc;
+        }
         e = prepare_slot(*sh.slot, (size_t)sh.rows * row_bytes, segments_out ? (size_t)sh.rows * seg_row_bytes : 0);
-        if (e != hipSuccess) return hip_fail(e, "workspace");
+        if (e == hipSuccess && progress) e = prepare_progress(*sh.slot, sh.rows);
+        if (e != hipSuccess) {
+            drain(k);
+            return hip_fail(e, "workspace");
+        }
         rc = render_async_impl(sc, cam, &sh.params, sh.slot->out_ws, segments_out ? sh.slot->seg_ws : nullptr, nullptr,
-                               sh.slot->stream);
-        if (rc) {  // let what is already enqueued finish before the slots can be reused
-            for (int32_t j = 0; j <= k; ++j)
-                if (shards[(size_t)j].rows > 0 && shards[(size_t)j].slot->stream) {
-                    (void)hipSetDevice(shards[(size_t)j].device);
-                    (void)hipStreamSynchronize(shards[(size_t)j].slot->stream);
-                }
+                               sh.slot->stream, 1, progress ? sh.slot->prog_dev : nullptr);
+        if (rc) {
+            drain(k + 1);
             return rc;
         }
     }
-    // Every shard is rendering; scatter each shard's compact rows into image order
-    // (shard k's i-th row is row k + i * n of the row set) with one strided copy each.
+    // With progress, every shard's counters are polled until all the renders
+    // are done, before the copies (a copy into pageable memory blocks).
+    int32_t reported = 0;
+    if (progress) {
+        std::vector<ProgressWatch> ws;
+        for (const Shard& sh : shards)
+            if (sh.rows > 0)
+                ws.push_back(ProgressWatch{sh.device, sh.slot, sh.rows,
+                                           (uint64_t)p->width * (uint64_t)p->rays_per_pixel, {}});
+        reported = poll_progress(ws, progress, user, e);
+    }
+    // Scatter each shard's compact rows into image order (shard k's i-th row is
+    // row k + i * n of the row set) with one strided copy each.
     for (int32_t k = 0; k < n_devices && e == hipSuccess; ++k) {
         const Shard& sh = shards[(size_t)k];
         if (sh.rows == 0) continue;
@@ -795,11 +884,14 @@ int tray_render_devices(const tray_sphere* spheres, int32_t n, const tray_backgr
         const hipError_t s2 = hipStreamSynchronize(sh.slot->stream);
         if (e == hipSuccess) e = s2;
     }
-    return e == hipSuccess ? TRAY_OK : hip_fail(e, "render");
+    if (e != hipSuccess) return hip_fail(e, "render");
+    report_rest(progress, user, rows, reported);
+    return TRAY_OK;
 }
 
 int tray_linear_to_srgba_async(const double* rgb_device, size_t n_pixels, uint8_t* rgba_device, int32_t device,
                                void* stream) {
+    if (g_in_progress_callback) return refuse_reentry("tray_linear_to_srgba_async");
     if ((!rgb_device || !rgba_device) && n_pixels) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     DeviceState* st = nullptr;
     int rc = device_state(device, &st);
@@ -823,28 +915,42 @@ int tray_linear_to_srgba_async(const double* rgb_device, size_t n_pixels, uint8_
     return TRAY_OK;
 }
 
-int tray_shutdown(void) {
-    std::lock_guard<std::mutex> lk(g_devices_mu);
-    for (size_t d = 0; d < g_devices.size(); ++d) {
-        DeviceState* st = g_devices[d];
-        if (!st) continue;
-        std::lock_guard<std::mutex> lk2(st->mu);
-        (void)hipSetDevice((int)d);
-        for (Slot& sl : st->slots) {
-            if (sl.stream) (void)hipStreamSynchronize(sl.stream);
-            if (sl.cached) tray_scene_release(sl.cached);
-            if (sl.out_ws) (void)hipFree(sl.out_ws);
-            if (sl.seg_ws) (void)hipFree(sl.seg_ws);
-            if (sl.stream) (void)hipStreamDestroy(sl.stream);
-        }
-        st->slots.clear();
-        if (st->prog_host) (void)hipHostFree(st->prog_host);
-        if (st->srgb) (void)hipFree(st->srgb);
-        st->prog_dev = nullptr;
-        st->prog_host = nullptr;
-        st->srgb = nullptr;
-        st->prog_bytes = 0;
+// Frees what the synchronous entry points keep on device d (slots: cached
+// scene with its sample and candidate buffers, workspaces, streams, progress
+// counters; the sRGB table). Called with g_devices_mu held.
+static void release_device(size_t d) {
+    DeviceState* st = g_devices[d];
+    if (!st) return;
+    std::lock_guard<std::mutex> lk2(st->mu);
+    (void)hipSetDevice((int)d);
+    for (Slot& sl : st->slots) {
+        if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+        if (sl.cached) tray_scene_release(sl.cached);
+        if (sl.out_ws) (void)hipFree(sl.out_ws);
+        if (sl.seg_ws) (void)hipFree(sl.seg_ws);
+        if (sl.prog_host) (void)hipHostFree(sl.prog_host);
+        if (sl.stream) (void)hipStreamDestroy(sl.stream);
     }
+    st->slots.clear();
+    if (st->srgb) (void)hipFree(st->srgb);
+    st->srgb = nullptr;
+}
+
+int tray_release_cache(int32_t device) {
+    if (g_in_progress_callback) return refuse_reentry("tray_release_cache");
+    std::lock_guard<std::mutex> lk(g_devices_mu);
+    if (device < 0) {
+        for (size_t d = 0; d < g_devices.size(); ++d) release_device(d);
+        return TRAY_OK;
+    }
+    if ((size_t)device < g_devices.size()) release_device((size_t)device);
+    return TRAY_OK;
+}
+
+int tray_shutdown(void) {
+    if (g_in_progress_callback) return refuse_reentry("tray_shutdown");
+    std::lock_guard<std::mutex> lk(g_devices_mu);
+    for (size_t d = 0; d < g_devices.size(); ++d) release_device(d);
     return TRAY_OK;
 }
 

@@ -767,12 +767,14 @@ __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D
 // count of its current tile row (wave-uniform `cur`, `cnt`) and adds it to the
 // host counter with one system-scope atomic when its lanes move on to another
 // tile row (a 64-item chunk lies within one tile row) and when it exits.
-__device__ __forceinline__ void flush_progress(const KernelParams& p, int32_t t, uint32_t n, uint32_t lane) {
+// 64-bit counts: a tile row holds 8 x width x rays_per_pixel samples, which can
+// pass 2^32 (e.g. width 4096 at r >= 131072).
+__device__ __forceinline__ void flush_progress(const KernelParams& p, int32_t t, uint64_t n, uint32_t lane) {
     if (n != 0u && lane == 0u)
-        __hip_atomic_fetch_add(p.progress + t, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_add(p.progress + t, (unsigned long long)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void count_progress(const KernelParams& p, bool ended, int32_t j, uint32_t lane,
-                                               int32_t& cur, uint32_t& cnt) {
+                                               int32_t& cur, uint64_t& cnt) {
     uint64_t m = __ballot(ended);
     while (m != 0ull) {
         const uint32_t first = (uint32_t)__builtin_ctzll(m);
@@ -783,7 +785,7 @@ __device__ __forceinline__ void count_progress(const KernelParams& p, bool ended
             cur = t0;
             cnt = 0u;
         }
-        cnt += (uint32_t)__popcll(same);
+        cnt += (uint64_t)__popcll(same);
         m &= ~same;
     }
 }
@@ -1063,7 +1065,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     uint32_t gcls = 0;  // diagnostic: class of the lane's current segment (1/2: from an out-of-tree sphere, up / other)
 #endif
     int32_t prog_cur = 0;  // live progress: the wave's current tile row and its unflushed count
-    uint32_t prog_cnt = 0;
+    uint64_t prog_cnt = 0;
 #ifdef TRAY_PROFILE
     __shared__ unsigned long long prof_lds[16 * 16];
     unsigned long long* prof = prof_lds + 16 * (threadIdx.x / 64u);
@@ -1536,7 +1538,9 @@ __device__ __forceinline__ Beam pixel_beam(const KernelParams& p, double xa, dou
     const D3 s0 = add(add(p00, smul(pxv, 0.5 * (xa + xb))), smul(pyv, 0.5 * (ya + yb)));
     const D3 b0 = lens ? add(b.pos, smul(sub(s0, b.pos), p.focus_time)) : s0;
     const double lx = __builtin_sqrt(length_sq(pxv)), ly = __builtin_sqrt(length_sq(pyv));
-    const double aa = (p.spp > 1 ? p.ray_radius * __builtin_sqrt(lx * lx + ly * ly) : 0.0) +
+    // |RayRadius|: Go's RenderLines accepts a negative radius and InDisc(r) is
+    // symmetric (disc() scales by the signed r), so the disc's extent is |r|.
+    const double aa = (p.spp > 1 ? __builtin_fabs(p.ray_radius) * __builtin_sqrt(lx * lx + ly * ly) : 0.0) +
                       0.5 * (xb - xa) * lx + 0.5 * (yb - ya) * ly;
     b.ra = lens ? __builtin_sqrt(length_sq(du) + length_sq(dv)) : 0.0;
     b.rb = lens ? aa * __builtin_fabs(p.focus_time) : aa;

@@ -102,7 +102,7 @@ struct KernelParams {
     void* out;
     uint32_t* segments;
     const double* srgb;  // TRAY_OUT_RGBA8: the 256-entry encoder table (tray::srgb_thresholds)
-    uint32_t* progress;  // nullable, HOST-mapped: samples finished per 8-row tile row of the compact rows
+    unsigned long long* progress;  // nullable, HOST-mapped: samples finished per 8-row tile row of the compact rows
     const uint4* cand;   // nullable (BVH only): primary-ray candidate record per compact pixel (launch_cand_build)
 };
 

@@ -262,11 +262,9 @@ class Tracer:  # ray/tracer.go:25-36
             def progress(rows):
                 for _ in range(rows):
                     self.ProgressFunc(self.width)
-        if self.Devices and len(self.Devices) > 1:  # one process, several GPUs (progress after the render)
+        if self.Devices and len(self.Devices) > 1:  # one process, several GPUs, live progress from all of them
             rgb, seg = _lib.render_devices(scene.to_array(), _background(scene.Background), self.Camera._state,
-                                           params, list(self.Devices), segments=True)
-            if progress is not None:
-                progress(y1 - y0)
+                                           params, list(self.Devices), segments=True, progress=progress)
         else:
             rgb, seg = _lib.render(scene.to_array(), _background(scene.Background), self.Camera._state, params,
                                    self.Devices[0] if self.Devices else self.Device, segments=True,
