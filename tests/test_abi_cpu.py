@@ -274,3 +274,30 @@ def test_import_order_library_before_torch():
     import torch
 
     assert n == "1" and os.path.realpath(path).startswith(os.path.realpath(os.path.dirname(torch.__file__))), path
+
+
+def test_host_go_tan_against_independent_restatement(L):
+    """The host's copy of Go's math.Tan (tray_host.cpp, Camera.Initialize's
+    viewport height, ray/camera.go:93) against the independent Python
+    restatement in tests/golden/make_golden.py, bit for bit. With the camera at
+    the origin looking down -z (up y), focal length 0.5 and a 1x1 image,
+    pixel_y = (0, -2 * 0.5 * tan(theta / 2), 0) exactly, so -pixel_y[1] IS the
+    host's go_tan(vfov * Pi/180 / 2)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden
+
+    deg = float.fromhex("0x1.1df46a2529d39p-6")  # Go's math.Pi / 180
+    rng = np.random.default_rng(11)
+    fovs = np.concatenate([rng.uniform(1e-3, 179.999, 3000), np.arange(1, 180, dtype=np.float64), [90.0, 20.0]])
+    for fov in fovs:
+        setup = _setup(L, np.array([0, 0, 0, 0, 0, 0, 0, 0, 0, float(fov), 0.5, 0, 0.0]))
+        st = L.CameraState()
+        L.check(L.lib().tray_camera_initialize(ctypes.byref(setup), 1, 1, ctypes.byref(st)))
+        assert st.pixel_y[0] == 0.0 and st.pixel_y[2] == 0.0
+        assert -st.pixel_y[1] == make_golden.go_tan(float(fov) * deg / 2.0), fov
+    st = L.CameraState()
+    setup = _setup(L, np.array([0, 0, 0, 0, 0, 0, 0, 0, 0, 90.0, 0.5, 0, 0.0]))
+    L.check(L.lib().tray_camera_initialize(ctypes.byref(setup), 1, 1, ctypes.byref(st)))
+    assert -st.pixel_y[1] == 1.0  # Go's tan(Pi/4) = 1 (libm: 1 - 2^-53)

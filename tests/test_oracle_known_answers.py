@@ -241,7 +241,8 @@ def test_get_ray_pixel_center_and_offset(O):  # ray/camera_test.go:177-243
 def test_go_math_tan_restatement(O):
     """Camera.Initialize's math.Tan (ray/camera.go:93) is Go's Cephes-based
     algorithm, not libm's: the C restatement (oracle; the host copy is checked
-    against the oracle through tray_camera_initialize) equals the independent
+    against the same Python restatement by test_abi_cpu.py::
+    test_host_go_tan_against_independent_restatement) equals the independent
     Python restatement in tests/golden/make_golden.py bit for bit, stays within
     2 ulp of the correctly rounded tangent, and reproduces Go's own
     tan(Pi/4) = 1 where libm gives 1 - 2^-53."""

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--linear", action="store_true", help="force the linear-scan kernel")
     ap.add_argument("--half", type=int, default=None, help="override the scene's grid half-extent (density)")
     ap.add_argument("--spp", type=int, default=None, help="override rays per pixel")
+    ap.add_argument("--passes", type=int, default=1,
+                    help="frames per launch (tray_render_passes_async; bench.py's launch shape is 16)")
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
     import numpy as np
@@ -65,15 +67,19 @@ def main():
         path = os.path.abspath(path)
         with _env(env):
             scene = _lib.DeviceScene(spheres, bg, 0, path)
-        runs[name] = dict(scene=scene, env=env, out=torch.empty((H, W, 3), dtype=torch.float32, device="cuda"),
-                          ms=[])
+        runs[name] = dict(scene=scene, env=env,
+                          out=torch.empty((args.passes, H, W, 3), dtype=torch.float32, device="cuda"), ms=[])
     ref = None
     for r in range(args.rounds + 1):
         for name, st in runs.items():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             with _env(st["env"]):
                 a.record(stream)
-                st["scene"].render_async(cam._state, params, st["out"].data_ptr(), None, stream.cuda_stream)
+                if args.passes == 1:
+                    st["scene"].render_async(cam._state, params, st["out"].data_ptr(), None, stream.cuda_stream)
+                else:
+                    st["scene"].render_passes_async(cam._state, params, args.passes, st["out"].data_ptr(),
+                                                    stream.cuda_stream)
                 b.record(stream)
             torch.cuda.synchronize()
             if r > 0:
@@ -82,11 +88,13 @@ def main():
                 ref = st["out"].clone()
             elif r == 0:
                 st["equal_to_first"] = bool(torch.equal(ref, st["out"]))
-    samples = W * H * spp
+    samples = W * H * spp * args.passes
     for name, st in runs.items():
         med = float(np.median(st["ms"]))
-        print(json.dumps({"variant": name, "median_ms": round(med, 3), "min_ms": round(min(st["ms"]), 3),
-                          "mrays": round(samples / med / 1e3, 1), "equal_to_first": st.get("equal_to_first", True)}))
+        print(json.dumps({"variant": name, "config": args.config, "passes": args.passes, "median_ms": round(med, 3),
+                          "min_ms": round(min(st["ms"]), 3), "ms_per_frame": round(med / args.passes, 4),
+                          "mrays": round(samples / med / 1e3, 1), "equal_to_first": st.get("equal_to_first", True)}),
+              flush=True)
 
 
 if __name__ == "__main__":

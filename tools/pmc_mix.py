@@ -24,7 +24,9 @@ def main():
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"]
             # the timed kernel: render_kernel<mode, true, false (no stats), spill>
-            if "render_kernel<" not in name or "<1, true, false, false, false>" not in name:  # the timed BVH kernel
+            # the timed BVH kernel: render_kernel<layout, true, false (no stats), false (no spill), false>
+            # (layout 1 for the book cover, 2 for the dense C5 scene)
+            if "render_kernel<" not in name or ", true, false, false, false>" not in name:
                 continue
             kernel = name
             key = (row["Counter_Name"], row["Dispatch_Id"])

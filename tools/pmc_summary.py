@@ -15,13 +15,15 @@ import json
 import os
 import shutil
 import statistics
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "tray::render_kernel<1, true, false, false, false>"
+KERNEL = ", true, false, false, false>"  # the timed BVH kernel, any LDS layout (1: book cover, 2: dense C5)
 
 
 def values(path):
-    rows = [r for r in csv.DictReader(open(path)) if KERNEL in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(path)) if "tray::render_kernel<" in r["Kernel_Name"] and
+            KERNEL in r["Kernel_Name"]]
     # drop the first launches of each slot: their buffers are cold (first touch)
     vals = [float(r["Counter_Value"]) for r in rows]
     return vals[len(vals) // 3:] if len(vals) >= 3 else vals
@@ -37,8 +39,18 @@ def main():
     d = args.profdir
     fetch_kb = statistics.median(values(os.path.join(d, "FETCH_SIZE", "pmc_counter_collection.csv")))
     write_kb = statistics.median(values(os.path.join(d, "WRITE_SIZE", "pmc_counter_collection.csv")))
-    fetch = fetch_kb * 1024 * 2
-    write = write_kb * 1024
+    # A launch of F frames runs in bands of <= 2^30 samples (tray_kernel.hip band_tile_rows), one
+    # megakernel dispatch each, and the counters are per dispatch: C2 is one band per 16-frame
+    # launch, C3/C5 several.
+    sys.path.insert(0, ROOT)
+    from bench import CONFIGS
+
+    _, _, _, W, H, spp, _ = CONFIGS[args.config]
+    tiles_x = (W + 7) // 8
+    band_rows = 8 * max(1, (1 << 30) // (tiles_x * 64 * spp * args.frames))
+    bands = -(-H // band_rows)
+    fetch = fetch_kb * 1024 * 2 * bands
+    write = write_kb * 1024 * bands
     copies = {
         os.path.join(d, "kt", "kt_kernel_stats.csv"): f"{args.tag}_kernel_stats.csv",
         os.path.join(d, "FETCH_SIZE", "pmc_counter_collection.csv"): f"{args.tag}_pmc_fetch_size.csv",
@@ -49,16 +61,18 @@ def main():
     rec = {
         "config": args.config,
         "frames_per_launch": args.frames,
-        "kernel": "tray::render_kernel<1, true, false, false, false> (BVH, whole scene in LDS, no stack spill)",
-        "FETCH_SIZE_KB_raw": fetch_kb,
-        "WRITE_SIZE_KB": write_kb,
+        "kernel": "tray::render_kernel<L, true, false, false, false> (BVH, LDS layout L, no stack spill)",
+        "bands_per_launch": bands,
+        "FETCH_SIZE_KB_raw_per_dispatch": fetch_kb,
+        "WRITE_SIZE_KB_per_dispatch": write_kb,
         "fetch_bytes_corrected": fetch,
         "write_bytes": write,
         "hbm_bytes_per_launch": int(fetch + write),
         "note": "megakernel only, per launch (frames_per_launch frames); its HBM traffic is the per-sample "
                 "colour buffer (24 B/sample). The resolve kernel reads it back.",
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md HBM "
-                  "section: FETCH_SIZE x2 on gfx950, WRITE_SIZE exact); median over the warm launches",
+                  "section: FETCH_SIZE x2 on gfx950, WRITE_SIZE exact); median over the warm dispatches x "
+                  "bands_per_launch",
         "source": [f"profiles/{v}" for v in list(copies.values())[1:]],
     }
     with open(os.path.join(ROOT, "profiles", f"pmc_{args.config}.json"), "w") as f:

@@ -86,6 +86,26 @@ __device__ __forceinline__ double div_rcp(double a, double b, double y) {
     if (__builtin_expect(!ok, 0)) return a / b;
     return q;
 }
+// A root of Sphere.Hit, (h -+ sqrt(disc)) / a (ray/objects.go:91,93), where the
+// only use of the quotient is `root > 1e-6 && root < closest` and, when that
+// holds, the value itself: a quotient below 2^-960 (or a zero of either sign)
+// fails root > 1e-6 whether or not it is exact, so only the upper end of
+// div_rcp_try's range check remains (q >= 2^960, infinities and NaN take the
+// full division). Two integer instructions instead of div_rcp_try's zero test,
+// range check and select.
+#ifndef TRAY_DIV_ROOT
+#define TRAY_DIV_ROOT 1
+#endif
+__device__ __forceinline__ double div_root(double a, double b, double y) {
+#if !TRAY_DIV_ROOT
+    return div_rcp(a, b, y);
+#endif
+    const double q = a * y;
+    const double r = __builtin_fma(-b, q, a);
+    const double q1 = __builtin_fma(r, y, q);
+    if (__builtin_expect((hi_word(q) & 0x7FF00000u) >= (1983u << 20), 0)) return a / b;
+    return q1;
+}
 __device__ __forceinline__ D3 sdiv_rcp(D3 v, double t, double y) {
     bool ok = true;
     const D3 q = d3(div_rcp_try(v.x, t, y, ok), div_rcp_try(v.y, t, y, ok), div_rcp_try(v.z, t, y, ok));
@@ -250,10 +270,10 @@ __device__ __forceinline__ void candidate(double h, double disc, double a, doubl
                                           int& best) {
     if (disc >= 0) {
         const double sq = sqrt_cr(disc);
-        double root = div_rcp(h - sq, a, a_inv);
+        double root = div_root(h - sq, a, a_inv);
         bool ok = root > 1e-6 && root < closest;
         if (!ok) {
-            root = div_rcp(h + sq, a, a_inv);
+            root = div_root(h + sq, a, a_inv);
             ok = root > 1e-6 && root < closest;
         }
         if (ok) {
@@ -263,23 +283,11 @@ __device__ __forceinline__ void candidate(double h, double disc, double a, doubl
     }
 }
 
-// The same decision for an out-of-order visit. Sphere.Hit's root choice does
-// not depend on the interval end: root2 >= root1, so the reference takes
-// t = root1 if root1 > 1e-6, else root2, and accepts it iff t < closestSoFar.
-// The linear scan therefore returns min over spheres of (t_i, i); accepting
-// "t < closest, or t == closest with a lower index" reproduces it for any order.
-__device__ __forceinline__ void candidate_any_order(double h, double disc, double a, double a_inv, int idx,
-                                                    double& closest, int& best) {
-    if (disc >= 0) {
-        const double sq = sqrt_cr(disc);
-        const double r1 = div_rcp(h - sq, a, a_inv);
-        const double t = r1 > 1e-6 ? r1 : div_rcp(h + sq, a, a_inv);
-        if (t > 1e-6 && (t < closest || (t == closest && idx < best))) {
-            closest = t;
-            best = idx;
-        }
-    }
-}
+// The any-order rule (test_geo). Sphere.Hit's root choice does not depend on
+// the interval end: root2 >= root1, so the reference takes t = root1 if
+// root1 > 1e-6, else root2, and accepts it iff t < closestSoFar. The linear
+// scan therefore returns min over spheres of (t_i, i); accepting "t < closest,
+// or t == closest with a lower index" reproduces it for any visiting order.
 
 // 17 FP64 add/mul per sphere, op order of Sphere.Hit (ray/objects.go:82-86).
 __device__ __forceinline__ void quad(const double4 g, const D3& org, const D3& dir, double a, double& h,
@@ -385,8 +393,7 @@ struct Trav {
     uint32_t top;                     // stack top: sort key (entry distance | reference)
     int32_t sp;                       // stack depth (the top included)
     double a, a_inv, closest;
-    int32_t best;  // original list index of the closest hit (tie-break key)
-    int32_t slot;  // its leaf slot (geometry + shading record)
+    int32_t slot;  // leaf slot (geometry + shading record) of the closest hit, -1: none
 };
 
 // The BVH kernel runs one workgroup per CU by default (all its waves share one
@@ -439,15 +446,28 @@ __device__ __forceinline__ float key_tn(uint32_t key) { return __uint_as_float(k
 __device__ __forceinline__ bool is_trav(uint32_t cur) { return cur < kBvhLeafBit; }
 __device__ __forceinline__ bool is_leaf(uint32_t cur) { return cur - kBvhLeafBit < kBvhNone - kBvhLeafBit; }
 
-// Sphere.Hit of the sphere in leaf slot `slot` under the any-order rule.
-__device__ __forceinline__ void test_slot(Trav& T, const SceneView& sv, int32_t slot, const D3& org, const D3& dir) {
+// Sphere.Hit of the sphere with geometry `g` in leaf slot `slot` under the
+// any-order rule (above) with the hit kept as a slot: the
+// original list index (the tie-break key, bidx) is read only on an exact tie
+// t == closest, which is rare, so no index load sits on the path of every
+// accepted hit (for scenes whose geometry stays in global memory it was a
+// second dependent round trip after the sphere's own load).
+__device__ __forceinline__ void test_geo(Trav& T, const SceneView& sv, const double4 g, int32_t slot, const D3& org,
+                                         const D3& dir) {
     double h, d;
-    quad(sv.bgeo[slot], org, dir, T.a, h, d);
+    quad(g, org, dir, T.a, h, d);
     if (d >= 0) {
-        const int32_t before = T.best;
-        candidate_any_order(h, d, T.a, T.a_inv, sv.bidx[slot], T.closest, T.best);
-        if (T.best != before) T.slot = slot;
+        const double sq = sqrt_cr(d);
+        const double r1 = div_root(h - sq, T.a, T.a_inv);
+        const double t = r1 > 1e-6 ? r1 : div_root(h + sq, T.a, T.a_inv);
+        if (t > 1e-6 && (t < T.closest || (t == T.closest && T.slot >= 0 && sv.bidx[slot] < sv.bidx[T.slot]))) {
+            T.closest = t;
+            T.slot = slot;
+        }
     }
+}
+__device__ __forceinline__ void test_slot(Trav& T, const SceneView& sv, int32_t slot, const D3& org, const D3& dir) {
+    test_geo(T, sv, sv.bgeo[slot], slot, org, dir);
 }
 
 // Scene.Hit's FP64 setup for a new segment: a = |dir|^2 and its reciprocal,
@@ -457,8 +477,7 @@ __device__ __forceinline__ void trav_globals(Trav& T, const SceneView& sv, const
     T.a = length_sq(dir);  // hoisted: same bits as per sphere
     T.a_inv = rcp_cr(T.a);
     T.closest = __builtin_inf();
-    T.best = -1;
-    T.slot = 0;
+    T.slot = -1;
 #pragma unroll
     for (int32_t g = 0; g < kBvhGlobals; ++g)
         if (g < sv.n_global) test_slot(T, sv, sv.global_first + g, org, dir);
@@ -630,11 +649,17 @@ __device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const St
         tested = 1;
     } else {
         const int32_t info = sv.leaves[T.cur & (kBvhLeafBit - 1u)];
-        const int32_t first = info >> 3, end = first + (info & 7);
+        const int32_t first = info >> 3, cnt = info & 7;
         tested = 0;
-        for (int32_t slot = first; slot < end; ++slot) {
-            test_slot(T, sv, slot, org, dir);
-            ++tested;
+        // Two spheres per step, both loads issued before either test: with the
+        // geometry in global memory (dense scenes) a leaf's spheres are then one
+        // L2 round trip, not one each. The second of an odd leaf reloads the first.
+        for (int32_t k = 0; k < cnt; k += 2) {
+            const int32_t s0 = first + k, s1 = k + 1 < cnt ? s0 + 1 : s0;
+            const double4 g0 = sv.bgeo[s0], g1 = sv.bgeo[s1];
+            test_geo(T, sv, g0, s0, org, dir);
+            if (s1 != s0) test_geo(T, sv, g1, s1, org, dir);
+            tested += s1 != s0 ? 2u : 1u;
         }
     }
     T.tlim = f32_up(T.closest);
@@ -939,6 +964,15 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         }                                                                     \
     }
 
+// ISA census build only (-DTRAY_CENSUS, tools/isa_census.py): a comment in the
+// assembly where each phase of the BVH loop starts, so the census can attribute
+// instructions to phases. Never in a timed build.
+#ifdef TRAY_CENSUS
+#define TRAY_MARK(name) asm volatile(";@phase " name);
+#else
+#define TRAY_MARK(name)
+#endif
+
 // Diagnostic build only (-DTRAY_PROFILE): per-wave s_memtime stamps around each
 // phase of the BVH loop, plus phase and active-lane counts, added into
 // stats[3..21] (the stats buffer must then hold 22 counters). Never part of a
@@ -1080,6 +1114,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #endif
         // Refill idle lanes from the wave's pool, fetching 64-item chunks from the global queue.
         PROF_T0();
+        TRAY_MARK("refill_assign")
         uint64_t idle = __ballot(!L.busy);
         if (__popcll(idle) < TRAY_REFILL_BATCH && idle != ~0ull) idle = 0ull;  // batch refills
         // Items are assigned first (cheap, may span two chunks); the camera rays of
@@ -1122,6 +1157,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         const uint64_t prof_assigned = __builtin_amdgcn_s_memtime();
 #endif
         if (fresh_item != ~0u) {
+            TRAY_MARK("refill_cam")
             int32_t x, j;
             uint32_t smp, pass;
             if (fresh_item < p.items && decode_item(p, fresh_item, x, j, smp, pass)) {
@@ -1147,6 +1183,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 }
 #endif
                 if constexpr (kBVH) {
+                    TRAY_MARK("refill_cand")
                     ++L.segments;
                     T.tlim = __builtin_inff();
                     trav_globals(T, sv, L.org, L.dir);
@@ -1184,10 +1221,11 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         // shade batch; the traversal lanes' batching is unchanged.
         if constexpr (kBVH) {
             if (__ballot(cam_hit) != 0ull) {
+                TRAY_MARK("refill_shade")
                 bool ended = false;
                 if (cam_hit) {
-                    if (shade_step<kStats>(p, uni, L, T.best, T.closest, T.a, [&] { return sv.bgeo[T.slot]; },
-                                           [&] { return sv.bmat[T.slot]; }, st)) {
+                    if (shade_step<kStats>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
+                                           [&] { return sv.bmat[max(T.slot, 0)]; }, st)) {
                         ++L.segments;
                         trav_begin(T, sv, L.org, L.dir);
                         if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
@@ -1230,6 +1268,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         }
 #endif
         PROF_ADD(0);
+        TRAY_MARK("refill_end")
         if (__ballot(L.busy) == 0ull) {
             if (exhausted) break;
             continue;              // every lane drew a padding item: draw again
@@ -1249,6 +1288,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             // Node steps for the traversing lanes.
             {
                 PROF_T0();
+                TRAY_MARK("node_ctl")
 #pragma unroll 1
                 for (int s = 0; s < TRAY_NODE_STEPS_MAX; ++s) {
                     const uint64_t m = __ballot(is_trav(T.cur));
@@ -1259,6 +1299,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     PROF_CNT(11, __popcll(__ballot(is_leaf(T.cur))));             // waiting for the leaf phase
                     PROF_CNT(12, __popcll(__ballot(L.busy && T.cur == kBvhNone)));  // waiting for the shade phase
                     if (is_trav(T.cur)) {
+                        TRAY_MARK("node")
                         uint32_t tested;
 #ifdef TRAY_PROBE_NODE
                         TRAY_PROBE_F32(TRAY_PROBE_NODE)
@@ -1281,6 +1322,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     }
                 }
                 PROF_ADD(1);
+                TRAY_MARK("leaf_decide")
             }
             // Leaf phase: FP64 sphere tests, batched.
             const uint64_t m_leaf = __ballot(is_leaf(T.cur));
@@ -1288,9 +1330,11 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             if (m_leaf != 0ull && (__popcll(m_leaf) >= TRAY_LEAF_BATCH || n_trav == 0u ||
                                    (n_trav < TRAY_TRAV_SPARSE && __popcll(m_leaf) >= TRAY_LEAF_LOW))) {
                 PROF_T0();
+                TRAY_MARK("leaf_ctl")
                 PROF_CNT(6, 1);
                 PROF_CNT(7, __popcll(m_leaf));
                 if (is_leaf(T.cur)) {
+                    TRAY_MARK("leaf")
                     uint32_t tested;
 #ifdef TRAY_PROBE_LEAF
                     TRAY_PROBE_F32(TRAY_PROBE_LEAF)
@@ -1319,22 +1363,24 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                                     (__popcll(__ballot(is_trav(T.cur))) < TRAY_TRAV_SPARSE &&
                                      __popcll(m_shade) >= TRAY_SHADE_LOW))) {
                 PROF_T0();
+                TRAY_MARK("shade_ctl")
                 PROF_CNT(8, 1);
                 PROF_CNT(9, __popcll(m_shade));
                 bool ended = false;
                 if (L.busy && T.cur == kBvhNone) {
+                    TRAY_MARK("shade")
 #ifdef TRAY_PROBE_SHADE
                     TRAY_PROBE_F32(TRAY_PROBE_SHADE)
 #endif
 #ifdef TRAY_PROBE_SHADE64
                     TRAY_PROBE_F64(TRAY_PROBE_SHADE64)
 #endif
-                    if (shade_step<kStats>(p, uni, L, T.best, T.closest, T.a, [&] { return sv.bgeo[T.slot]; },
-                                           [&] { return sv.bmat[T.slot]; }, st)) {
+                    if (shade_step<kStats>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
+                                           [&] { return sv.bmat[max(T.slot, 0)]; }, st)) {
                         ++L.segments;
 #if defined(TRAY_STATS_GROUND) && !defined(TRAY_PROFILE)
                         {
-                            const bool from_g = T.best >= 0 && T.slot >= sv.global_first;
+                            const bool from_g = T.slot >= sv.global_first;
                             const bool up = L.dir.y >= __builtin_fmax(__builtin_fabs(L.dir.x), __builtin_fabs(L.dir.z));
                             gcls = from_g ? (up ? 1u : 2u) : 0u;
                             if constexpr (kStats) {
@@ -1351,6 +1397,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 }
                 if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
                 PROF_ADD(3);
+                TRAY_MARK("shade_end")
             }
         }
     }
