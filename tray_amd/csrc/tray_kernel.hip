@@ -55,62 +55,41 @@ __device__ __forceinline__ D3 neg(D3 v) { return d3(-v.x, -v.y, -v.z); }
 // a / b, correctly rounded, given y = RN(1/b) (exactly rounded, e.g. a full
 // division or a host-side 1.0/b): q = RN(a*y) is within 1 ulp of a/b, the
 // residual fma(-b, q, a) is exact, and one correction fma(r, y, q) returns
-// RN(a/b) (Markstein 1990; Muller et al., Handbook of Floating-Point Arithmetic
-// §4.7). 3 FP64 instructions instead of ~10 for the generic sequence; checked
-// on 10^9 pairs by tools/div_check.hip. Zero keeps its sign, and quotients near
-// the overflow/underflow range (or non-finite operands) take the full division.
-// Branch-free form: `ok` is cleared when the quotient needs the full division
-// (the caller then redoes its divisions in one rarely taken branch).
-#ifndef TRAY_INT_RANGE
-#define TRAY_INT_RANGE 1
-#endif
-
-__device__ __forceinline__ double div_rcp_try(double a, double b, double y, bool& ok) {
+// RN(a/b) when |q| lies in [2^-960, 2^960) (Markstein 1990; Muller et al.,
+// Handbook of Floating-Point Arithmetic §4.7). 3 FP64 instructions instead of
+// ~10 for the generic sequence; checked on 4.3e9 pairs by tools/div_check.hip.
+// The range is tested on the high word (biased exponent 63..1982; NaN and
+// infinities fail); quotients outside it take the full division in a rarely
+// taken branch.
+//
+// A vector divided by t (Unit, the normal (P - C) / R): one range check per
+// component and one branch for the three. A zero component also takes that
+// branch (the sign of a zero quotient needs the full division; exact zeros do
+// not occur in practice), so the common path has no zero test and no select.
+__device__ __forceinline__ double div_rcp_nz(double a, double b, double y, bool& ok) {
     const double q = a * y;
     const double r = __builtin_fma(-b, q, a);
-    const double q1 = __builtin_fma(r, y, q);
-    const bool a0 = a == 0;
-#if TRAY_INT_RANGE
-    // |q| in [2^-960, 2^960): biased exponent 63..1982, tested on the high word
-    // (bitwise, so no branches; NaN and infinities fail).
-    ok = ok & (a0 | (((hi_word(q) & 0x7FF00000u) - (63u << 20)) < (1920u << 20)));
-#else
-    const double aq = __builtin_fabs(q);
-    ok = ok && (a0 || (aq > 0x1p-960 && aq < 0x1p+960));
-#endif
-    return a0 ? q : q1;
+    ok = ok & (((hi_word(q) & 0x7FF00000u) - (63u << 20)) < (1920u << 20));
+    return __builtin_fma(r, y, q);
 }
-__device__ __forceinline__ double div_rcp(double a, double b, double y) {
+__device__ __forceinline__ D3 sdiv_rcp(D3 v, double t, double y) {
     bool ok = true;
-    const double q = div_rcp_try(a, b, y, ok);
-    if (__builtin_expect(!ok, 0)) return a / b;
+    const D3 q = d3(div_rcp_nz(v.x, t, y, ok), div_rcp_nz(v.y, t, y, ok), div_rcp_nz(v.z, t, y, ok));
+    if (__builtin_expect(!ok, 0)) return sdiv(v, t);
     return q;
 }
-// A root of Sphere.Hit, (h -+ sqrt(disc)) / a (ray/objects.go:91,93), where the
-// only use of the quotient is `root > 1e-6 && root < closest` and, when that
-// holds, the value itself: a quotient below 2^-960 (or a zero of either sign)
-// fails root > 1e-6 whether or not it is exact, so only the upper end of
-// div_rcp_try's range check remains (q >= 2^960, infinities and NaN take the
-// full division). Two integer instructions instead of div_rcp_try's zero test,
-// range check and select.
-#ifndef TRAY_DIV_ROOT
-#define TRAY_DIV_ROOT 1
-#endif
+// A root of Sphere.Hit, (h -+ sqrt(disc)) / a (ray/objects.go:91,93), is used
+// only through `root > 1e-6 && root < closest` and, when that holds, as the
+// value itself: a quotient below 2^-960 (or a zero of either sign) fails
+// root > 1e-6 whether or not it is exact, so only the upper end of the range
+// is checked (q >= 2^960, infinities and NaN take the full division): two
+// integer instructions and no select.
 __device__ __forceinline__ double div_root(double a, double b, double y) {
-#if !TRAY_DIV_ROOT
-    return div_rcp(a, b, y);
-#endif
     const double q = a * y;
     const double r = __builtin_fma(-b, q, a);
     const double q1 = __builtin_fma(r, y, q);
     if (__builtin_expect((hi_word(q) & 0x7FF00000u) >= (1983u << 20), 0)) return a / b;
     return q1;
-}
-__device__ __forceinline__ D3 sdiv_rcp(D3 v, double t, double y) {
-    bool ok = true;
-    const D3 q = d3(div_rcp_try(v.x, t, y, ok), div_rcp_try(v.y, t, y, ok), div_rcp_try(v.z, t, y, ok));
-    if (__builtin_expect(!ok, 0)) return sdiv(v, t);
-    return q;
 }
 __device__ __forceinline__ double dot(D3 u, D3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
 __device__ __forceinline__ double length_sq(D3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
@@ -244,12 +223,20 @@ __device__ __forceinline__ uint32_t srgba_word(const double* t, double r, double
     return srgb_encode(t, r) | (srgb_encode(t, g) << 8) | (srgb_encode(t, b) << 16) | (255u << 24);
 }
 
+// n / d and n % d by the launch's FastDiv (tray_kernel.hpp).
+__device__ __forceinline__ uint32_t udiv(uint32_t n, const FastDiv& f, uint32_t& rem) {
+    const uint32_t t = __umulhi(n, f.m);
+    const uint32_t q = (t + ((n - t) >> f.s1)) >> f.s2;
+    rem = n - q * f.d;
+    return q;
+}
+
 // Compact output row j -> image row y (see tray_params in include/tray.h).
 __device__ __forceinline__ int32_t row_of(const KernelParams& p, int32_t j) {
     if (p.tile_rows <= 0) return p.y_start + j;
-    const int32_t t = j / p.tile_rows;
-    const int32_t within = j - t * p.tile_rows;
-    return p.y_start + (t * p.tile_count + p.tile_index) * p.tile_rows + within;
+    uint32_t within;
+    const int32_t t = (int32_t)udiv((uint32_t)j, p.div_tile_rows, within);
+    return p.y_start + (t * p.tile_count + p.tile_index) * p.tile_rows + (int32_t)within;
 }
 
 // Per-lane path state. A lane owns one pixel at a time and walks its samples
@@ -717,23 +704,6 @@ __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni
 // Work item i of a band = one sample: pixel q = i / r in 8x8-tile order of the
 // band's compact rows (so a 64-item chunk is one pixel's samples at r = 64, or
 // an 8x8 tile at r = 1), sample s = i % r.
-// n / d for n < 2^32 through the FP64 reciprocal (rinv = RN(1/d)): the product
-// is within 2^-20 of n/d, so its floor is off by at most one; one correction step.
-__device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t d, double rinv, uint32_t& rem) {
-    // 0 <= n * rinv < 2^32: a single v_cvt_u32_f64 (an int64 conversion is ~10 instructions)
-    int64_t q = (int64_t)(uint32_t)((double)n * rinv);
-    int64_t r = (int64_t)n - q * (int64_t)d;
-    if (r < 0) {
-        --q;
-        r += d;
-    } else if (r >= (int64_t)d) {
-        ++q;
-        r -= d;
-    }
-    rem = (uint32_t)r;
-    return (uint32_t)q;
-}
-
 // With several progressive passes in the launch, item i is item i % frame_items
 // of pass i / frame_items (a 64-item chunk never straddles two passes:
 // frame_items is a multiple of 64). `k` returns the pass within the launch.
@@ -742,13 +712,13 @@ __device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, i
     k = 0;
     if (p.passes > 1) {
         uint32_t li;
-        k = udiv(i, p.frame_items, p.inv_frame_items, li);
+        k = udiv(i, p.div_frame_items, li);
         i = li;
     }
-    const uint32_t q = udiv(i, (uint32_t)p.spp, p.inv_spp, s);
+    const uint32_t q = udiv(i, p.div_spp, s);
     const uint32_t tile = q >> 6, r = q & 63u;
     uint32_t tx;
-    const uint32_t ty = udiv(tile, (uint32_t)p.tiles_x, p.inv_tiles_x, tx);
+    const uint32_t ty = udiv(tile, p.div_tiles_x, tx);
     x = (int32_t)(tx * 8u + (r & 7u));
     const int32_t jb = (int32_t)(ty * 8u + (r >> 3));
     j = p.j0 + jb;
@@ -1663,7 +1633,9 @@ size_t cand_workspace_bytes(int32_t width, int32_t rows) {
     return pixels * sizeof(uint4) + tiles * (kCandTileSlots * sizeof(uint16_t) + sizeof(uint32_t));
 }
 
-hipError_t launch_cand_build(const KernelParams& p, uint4* out, hipStream_t stream) {
+hipError_t launch_cand_build(const KernelParams& kp, uint4* out, hipStream_t stream) {
+    KernelParams p = kp;
+    p.div_tile_rows = make_fastdiv((uint32_t)std::max(p.tile_rows, 1));  // row_of
     const size_t n = (size_t)p.rows * (size_t)p.width;
     if (n == 0) return hipSuccess;
     const size_t tiles = (size_t)((p.width + 7) / 8) * (size_t)((p.rows + 7) / 8);
@@ -1823,8 +1795,9 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (!band_fits(p.width, spp_launch)) return hipErrorInvalidValue;
     if (p.segments && p.passes > 1) return hipErrorInvalidValue;
     p.tiles_x = (p.width + 7) / 8;
-    p.inv_spp = 1.0 / (double)p.spp;
-    p.inv_tiles_x = 1.0 / (double)p.tiles_x;
+    p.div_spp = make_fastdiv((uint32_t)p.spp);
+    p.div_tiles_x = make_fastdiv((uint32_t)p.tiles_x);
+    p.div_tile_rows = make_fastdiv((uint32_t)std::max(p.tile_rows, 1));
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -1902,7 +1875,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         p.band_rows = std::min(band, p.rows - j0);
         const uint32_t pixels = (uint32_t)p.tiles_x * (uint32_t)((p.band_rows + 7) / 8) * 64u;
         p.frame_items = pixels * (uint32_t)p.spp;
-        p.inv_frame_items = 1.0 / (double)p.frame_items;
+        p.div_frame_items = make_fastdiv(p.frame_items);
         p.items = p.frame_items * p.passes;
         p.nchunks = (p.items + 63u) / 64u;
         p.pool_chunks = std::min<uint32_t>(TRAY_POOL_CHUNKS, std::max<uint32_t>(16u, p.nchunks / (8u * (uint32_t)blocks)));

@@ -62,6 +62,25 @@ struct V3 {
 // branch-free three-entry push writes unconditionally (tray_kernel.hip trav_node).
 constexpr int32_t kStackSlack = 3;
 
+// Unsigned 32-bit division by a launch-invariant divisor d >= 1 (Granlund and
+// Montgomery 1994, the round-up method): with l = ceil(log2 d) and
+// m = floor(2^32 (2^l - d) / d) + 1, t = mulhi(n, m) gives
+// n / d = (t + ((n - t) >> min(l, 1))) >> max(l - 1, 0) for every n < 2^32.
+// Five integer instructions on the device, no FP64 conversion.
+struct FastDiv {
+    uint32_t d, m, s1, s2;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;
+    FastDiv f;
+    f.d = d;
+    f.m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    f.s1 = l < 1 ? l : 1;
+    f.s2 = l > 1 ? l - 1 : 0;
+    return f;
+}
+
 struct KernelParams {
     const double4* geo;  // n_pad entries: n spheres, then NaN padding (never hit)
     const MatRec* mat;
@@ -74,10 +93,10 @@ struct KernelParams {
     uint32_t items;      // band work items: passes x frame_items
     uint32_t frame_items;  // one pass's items of the band: 8x8-tile-padded pixels x spp
     uint32_t passes, pass0;  // progressive passes pass0 .. pass0 + passes - 1 in this launch
-    double inv_frame_items;  // RN(1/frame_items)
+    FastDiv div_frame_items;  // item -> (pass, item within the pass)
     size_t out_frame_bytes;  // output stride between passes
     int32_t j0, band_rows;  // the band: compact rows [j0, j0 + band_rows)
-    double inv_spp, inv_tiles_x;  // RN(1/spp), RN(1/tiles_x): item decoding
+    FastDiv div_spp, div_tiles_x, div_tile_rows;  // item decoding; compact row -> image row
     double* samples;     // per-item path colours (3 doubles), summed in order by the resolve kernel
     const Bvh4Node* nodes;  // exact-culling 4-wide BVH (tray_bvh.cpp), root first
     const int32_t* leaves;  // per leaf: (first slot << 3) | count
