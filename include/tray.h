@@ -309,6 +309,24 @@ int tray_to_srgba(const double *rgb, size_t n_pixels, uint8_t *rgba);
 int tray_linear_to_srgba_async(const double *rgb_device, size_t n_pixels, uint8_t *rgba_device, int32_t device,
                                void *stream);
 
+/* ---- the terminal view's downscale (main.go:119-128) ------------------------- */
+/* golang.org/x/image/draw (v0.35.0, go.mod:11) scalers, op Over: main.go scales the
+ * rendered image into a fresh (zero) image of the terminal's size. */
+typedef enum tray_scale_filter {
+    TRAY_SCALE_NEAREST = 0, /* draw.NearestNeighbor.Scale (main.go:125, supersample < 1) */
+    TRAY_SCALE_BILINEAR = 1 /* draw.BiLinear.Scale (main.go:127, supersample > 1) */
+} tray_scale_filter;
+
+/* Scales the RGBA8 image src (src_width x src_height, pitch 4 * src_width) onto
+ * dst (dst_width x dst_height), blending Over dst's current contents exactly as
+ * the Go scalers do, on `device`. Host buffers; synchronous. */
+int tray_scale_rgba(const uint8_t *src, int32_t src_width, int32_t src_height, uint8_t *dst, int32_t dst_width,
+                    int32_t dst_height, int32_t filter, int32_t device);
+/* The same over DEVICE buffers, enqueued on `stream` (e.g. a TRAY_OUT_RGBA8 frame
+ * still on the device: only the terminal-sized image need come back). */
+int tray_scale_rgba_async(const uint8_t *src_device, int32_t src_width, int32_t src_height, uint8_t *dst_device,
+                          int32_t dst_width, int32_t dst_height, int32_t filter, int32_t device, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

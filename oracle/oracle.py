@@ -86,6 +86,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_camera_initialize.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp]
         L.oracle_rich_scene.argtypes = [ctypes.c_uint64, ctypes.c_int, _vp, ctypes.c_int]
         L.oracle_default_scene.argtypes = [_vp, ctypes.c_int]
+        for fn in (L.oracle_scale_bilinear_rgba, L.oracle_scale_nearest_rgba):
+            fn.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, _vp, ctypes.c_int32, ctypes.c_int32]
         _lib = L
     return _lib
 
@@ -307,3 +309,16 @@ def ray_color(spheres, background, origin, direction, depth, seed=1, pixel=0, sa
     if rc != 0:
         raise ValueError("unsupported material")
     return out, seg.value
+
+
+# ------------------------------------------------------- terminal downscale --
+def scale_rgba(src: np.ndarray, dw: int, dh: int, bilinear: bool, dst: np.ndarray | None = None) -> np.ndarray:
+    """x/image/draw {BiLinear,NearestNeighbor}.Scale(dst, dst.Bounds(), src, src.Bounds(), Over, nil)
+    for [H, W, 4] uint8 images (main.go:121-128: dst is a fresh, zero image unless given)."""
+    a = np.ascontiguousarray(src, dtype=np.uint8)
+    sh, sw = a.shape[:2]
+    out = np.zeros((dh, dw, 4), dtype=np.uint8) if dst is None else np.ascontiguousarray(dst, dtype=np.uint8).copy()
+    fn = lib().oracle_scale_bilinear_rgba if bilinear else lib().oracle_scale_nearest_rgba
+    if fn(a.ctypes.data, sw, sh, out.ctypes.data, dw, dh) != 0:
+        raise ValueError("bad sizes")
+    return out

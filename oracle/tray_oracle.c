@@ -819,3 +819,166 @@ ORACLE_EXPORT int oracle_default_scene(o_sphere *out, int cap) {
     put_sphere(&out[4], V(1.0, 0, -1), 0.5, O_METAL, V(1, .8, .8), 0.05);
     return 5;
 }
+
+/* ------------------------------------------------------------------ */
+/* Terminal view downscale: main.go:119-128.   */
+/* ------------------------------------------------------------------ */
+/*
+ * main.go:121-128 scales the rendered *image.RGBA into a fresh image.NewRGBA
+ * (all zeros) of the terminal's size with draw.NearestNeighbor.Scale
+ * (supersample < 1) or draw.BiLinear.Scale (supersample > 1), op draw.Over.
+ * Both live in golang.org/x/image v0.35.0 (go.mod:11), which is NOT vendored
+ * in the reference: this restates the published algorithm of its draw package
+ * (scale.go: Kernel, newDistrib, kernelScaler.Scale; impl.go: the generated
+ * scaleX_RGBA / scaleY_RGBA_Over and nnInterpolator scale_RGBA_RGBA_Over for
+ * an *image.RGBA source and destination) in Go's op order, FP64, no FMA
+ * (GOAMD64=v1; Go on arm64 may fuse `a*b + c`). Parity with the library
+ * itself is UNPINNED (neither the module nor a fixture is in the tree).
+ * Images are RGBA8, row pitch 4*width; dst is blended onto (Over), as Go does.
+ */
+typedef struct {
+    int32_t i, j;             /* contribs[i..j) */
+    double inv_total;         /* 1 / total weight */
+    double inv_total_ffff;    /* (1 / total weight) / 0xffff */
+} o_source;
+typedef struct {
+    int32_t coord;
+    double weight;
+} o_contrib;
+
+/* BiLinear = &Kernel{Support: 1, At: func(t) { return 1 - t }}; newDistrib(q, dw, sw). */
+static int bilinear_distrib(int32_t dw, int32_t sw, o_source *sources, o_contrib *contribs, int32_t cap) {
+    const double support = 1.0;
+    const double scale = (double)sw / (double)dw;
+    double half_width = support, arg_scale = 1.0;
+    if (scale > 1) { /* shrinking: widen the support to visit every source pixel */
+        half_width *= scale;
+        arg_scale = 1 / scale;
+    }
+    int32_t n = 0;
+    for (int32_t x = 0; x < dw; ++x) {
+        const double center = ((double)x + 0.5) * scale - 0.5;
+        int32_t i = (int32_t)floor(center - half_width);
+        if (i < 0) i = 0;
+        int32_t j = (int32_t)ceil(center + half_width);
+        if (j > sw) {
+            j = sw;
+            if (j < i) j = i;
+        }
+        double total = 0.0;
+        const int32_t l = n;
+        for (int32_t coord = i; coord < j; ++coord) {
+            const double t = fabs((center - (double)coord) * arg_scale);
+            if (t >= support) continue;
+            const double w = 1 - t;
+            if (w == 0) continue;
+            if (n >= cap) return -1;
+            total += w;
+            contribs[n].coord = coord;
+            contribs[n].weight = w;
+            ++n;
+        }
+        total = 1 / total;
+        sources[x].i = l;
+        sources[x].j = n;
+        sources[x].inv_total = total;
+        sources[x].inv_total_ffff = total / 0xffff;
+    }
+    return n;
+}
+
+/* ftou (x/image/draw scale.go): int32(0xffff*f + 0.5) clamped to [0, 0xffff]. */
+static uint32_t go_ftou(double f) {
+    const double v = 0xffff * f + 0.5;
+    int32_t i;
+    if (!(v < 2147483648.0)) i = INT32_MAX; /* Go's int32(x) of a large float is implementation-defined; */
+    else if (!(v > -2147483649.0)) i = INT32_MIN; /* clamping keeps the result in range either way */
+    else i = (int32_t)v;
+    if (i > 0xffff) return 0xffff;
+    if (i > 0) return (uint32_t)i;
+    return 0;
+}
+
+static void over_px(uint8_t *d, uint32_t r, uint32_t g, uint32_t b, uint32_t a) {
+    const uint32_t a1 = (0xffff - a) * 0x101;
+    d[0] = (uint8_t)(((uint32_t)d[0] * a1 / 0xffff + r) >> 8);
+    d[1] = (uint8_t)(((uint32_t)d[1] * a1 / 0xffff + g) >> 8);
+    d[2] = (uint8_t)(((uint32_t)d[2] * a1 / 0xffff + b) >> 8);
+    d[3] = (uint8_t)(((uint32_t)d[3] * a1 / 0xffff + a) >> 8);
+}
+
+/* draw.BiLinear.Scale(dst, dst.Bounds(), src, src.Bounds(), draw.Over, nil). Returns 0, or -1. */
+ORACLE_EXPORT int oracle_scale_bilinear_rgba(const uint8_t *src, int32_t sw, int32_t sh, uint8_t *dst, int32_t dw,
+                                             int32_t dh) {
+    if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0) return -1;
+    /* every destination pixel takes at most ceil(2 * max(scale, 1)) + 1 taps */
+    const int32_t capx = dw * (2 * (sw / dw + 2) + 2), capy = dh * (2 * (sh / dh + 2) + 2);
+    o_source *hs = malloc(sizeof(o_source) * (size_t)dw), *vs = malloc(sizeof(o_source) * (size_t)dh);
+    o_contrib *hc = malloc(sizeof(o_contrib) * (size_t)capx), *vc = malloc(sizeof(o_contrib) * (size_t)capy);
+    double *tmp = malloc(sizeof(double) * 4 * (size_t)dw * (size_t)sh);
+    int rc = -1;
+    if (!hs || !vs || !hc || !vc || !tmp) goto out;
+    if (bilinear_distrib(dw, sw, hs, hc, capx) < 0 || bilinear_distrib(dh, sh, vs, vc, capy) < 0) goto out;
+    /* scaleX_RGBA: the source's columns distributed over tmp [sh][dw] */
+    for (int32_t y = 0; y < sh; ++y) {
+        for (int32_t x = 0; x < dw; ++x) {
+            double pr = 0, pg = 0, pb = 0, pa = 0;
+            for (int32_t k = hs[x].i; k < hs[x].j; ++k) {
+                const uint8_t *p = src + ((size_t)y * (size_t)sw + (size_t)hc[k].coord) * 4;
+                pr += (double)((uint32_t)p[0] * 0x101) * hc[k].weight;
+                pg += (double)((uint32_t)p[1] * 0x101) * hc[k].weight;
+                pb += (double)((uint32_t)p[2] * 0x101) * hc[k].weight;
+                pa += (double)((uint32_t)p[3] * 0x101) * hc[k].weight;
+            }
+            double *t = tmp + ((size_t)y * (size_t)dw + (size_t)x) * 4;
+            t[0] = pr * hs[x].inv_total_ffff;
+            t[1] = pg * hs[x].inv_total_ffff;
+            t[2] = pb * hs[x].inv_total_ffff;
+            t[3] = pa * hs[x].inv_total_ffff;
+        }
+    }
+    /* scaleY_RGBA_Over: tmp's rows distributed over dst, blended Over */
+    for (int32_t x = 0; x < dw; ++x) {
+        for (int32_t y = 0; y < dh; ++y) {
+            double pr = 0, pg = 0, pb = 0, pa = 0;
+            for (int32_t k = vs[y].i; k < vs[y].j; ++k) {
+                const double *t = tmp + ((size_t)vc[k].coord * (size_t)dw + (size_t)x) * 4;
+                pr += t[0] * vc[k].weight;
+                pg += t[1] * vc[k].weight;
+                pb += t[2] * vc[k].weight;
+                pa += t[3] * vc[k].weight;
+            }
+            if (pr > pa) pr = pa;
+            if (pg > pa) pg = pa;
+            if (pb > pa) pb = pa;
+            over_px(dst + ((size_t)y * (size_t)dw + (size_t)x) * 4, go_ftou(pr * vs[y].inv_total),
+                    go_ftou(pg * vs[y].inv_total), go_ftou(pb * vs[y].inv_total), go_ftou(pa * vs[y].inv_total));
+        }
+    }
+    rc = 0;
+out:
+    free(hs);
+    free(vs);
+    free(hc);
+    free(vc);
+    free(tmp);
+    return rc;
+}
+
+/* draw.NearestNeighbor.Scale(dst, dst.Bounds(), src, src.Bounds(), draw.Over, nil):
+ * source pixel ((2 dx + 1) sw / (2 dw), (2 dy + 1) sh / (2 dh)) in integers. */
+ORACLE_EXPORT int oracle_scale_nearest_rgba(const uint8_t *src, int32_t sw, int32_t sh, uint8_t *dst, int32_t dw,
+                                            int32_t dh) {
+    if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0) return -1;
+    const uint64_t dw2 = (uint64_t)dw * 2, dh2 = (uint64_t)dh * 2;
+    for (int32_t dy = 0; dy < dh; ++dy) {
+        const uint64_t sy = (2 * (uint64_t)dy + 1) * (uint64_t)sh / dh2;
+        for (int32_t dx = 0; dx < dw; ++dx) {
+            const uint64_t sx = (2 * (uint64_t)dx + 1) * (uint64_t)sw / dw2;
+            const uint8_t *p = src + ((size_t)sy * (size_t)sw + (size_t)sx) * 4;
+            over_px(dst + ((size_t)dy * (size_t)dw + (size_t)dx) * 4, (uint32_t)p[0] * 0x101, (uint32_t)p[1] * 0x101,
+                    (uint32_t)p[2] * 0x101, (uint32_t)p[3] * 0x101);
+        }
+    }
+    return 0;
+}

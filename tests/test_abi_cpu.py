@@ -301,3 +301,14 @@ def test_host_go_tan_against_independent_restatement(L):
     setup = _setup(L, np.array([0, 0, 0, 0, 0, 0, 0, 0, 0, 90.0, 0.5, 0, 0.0]))
     L.check(L.lib().tray_camera_initialize(ctypes.byref(setup), 1, 1, ctypes.byref(st)))
     assert -st.pixel_y[1] == 1.0  # Go's tan(Pi/4) = 1 (libm: 1 - 2^-53)
+
+
+def test_scale_argument_checks(L):
+    """tray_scale_rgba rejects bad sizes, filters and null images before any device work."""
+    img = np.zeros((4, 4, 4), np.uint8)
+    out = np.zeros((2, 2, 4), np.uint8)
+    lib = L.lib()
+    assert lib.tray_scale_rgba(img.ctypes.data, 4, 4, out.ctypes.data, 0, 2, 1, 0) == L.TRAY_ERR_INVALID_ARGUMENT
+    assert lib.tray_scale_rgba(img.ctypes.data, 4, 4, out.ctypes.data, 2, 2, 7, 0) == L.TRAY_ERR_INVALID_ARGUMENT
+    assert lib.tray_scale_rgba(None, 4, 4, out.ctypes.data, 2, 2, 1, 0) == L.TRAY_ERR_INVALID_ARGUMENT
+    assert lib.tray_scale_rgba_async(None, 4, 4, None, 2, 2, 0, 0, None) == L.TRAY_ERR_INVALID_ARGUMENT

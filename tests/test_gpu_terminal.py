@@ -1,0 +1,54 @@
+"""The terminal view's device scaler (tray_scale_rgba / tray_scale_rgba_async,
+main.go:119-128) against the oracle's restatement of golang.org/x/image/draw's
+BiLinear and NearestNeighbor scalers, byte for byte. Parity with the Go library
+itself is unpinned (not vendored; no fixture in the reference)."""
+import numpy as np
+import pytest
+
+from test_terminal_cpu import SIZES, rgba
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("src_hw,dst_hw", SIZES)
+def test_device_bilinear_equals_oracle(L, O, src_hw, dst_hw):
+    for opaque in (True, False):
+        img = rgba(*src_hw, seed=7 + sum(dst_hw), opaque=opaque)
+        got = L.scale_rgba(img, dst_hw[1], dst_hw[0], bilinear=True)
+        assert np.array_equal(got, O.scale_rgba(img, dst_hw[1], dst_hw[0], bilinear=True))
+    img = rgba(*src_hw, seed=5, opaque=False)
+    dst = rgba(*dst_hw, seed=6)  # Over blends onto what dst holds
+    assert np.array_equal(L.scale_rgba(img, dst_hw[1], dst_hw[0], True, dst=dst),
+                          O.scale_rgba(img, dst_hw[1], dst_hw[0], True, dst=dst))
+
+
+def test_device_nearest_equals_oracle(L, O):
+    for (sh, sw), (dh, dw) in [((12, 20), (45, 80)), ((3, 4), (6, 8)), ((7, 9), (50, 33)), ((90, 160), (45, 80))]:
+        img = rgba(sh, sw, seed=sh, opaque=False)
+        assert np.array_equal(L.scale_rgba(img, dw, dh, bilinear=False), O.scale_rgba(img, dw, dh, bilinear=False))
+
+
+def test_rendered_frame_to_terminal(L, O):
+    """main.go's path: a 4x-supersampled render of the book cover for a 40x12
+    terminal (160x96 RGBA8, rendered on the device), scaled to 40x24 on the
+    device straight from device memory (tray_scale_rgba_async), equal to the
+    oracle's scaling of the same frame; and through tray_amd.terminal."""
+    import torch
+
+    from tray_amd import ray, terminal
+
+    W, H = terminal.image_size(40, 12, 4)
+    cam = ray.RichSceneCamera()
+    cam.Initialize(W, H)
+    p = L.make_params(W, H, 20, 4, 0.5, 2, output=L.OUT_RGBA8)
+    frame, _ = L.render(ray.rich_scene_array(2), ray._background(ray.DefaultBackground()), cam._state, p)
+    ref = O.scale_rgba(frame, 40, 24, bilinear=True)
+    assert np.array_equal(terminal.scale_image(frame, 40, 24, 4), ref)
+    src = torch.from_numpy(frame).cuda()
+    dst = torch.zeros((24, 40, 4), dtype=torch.uint8, device="cuda")
+    L.check(L.lib().tray_scale_rgba_async(src.data_ptr(), W, H, dst.data_ptr(), 40, 24, L.SCALE_BILINEAR, 0,
+                                          torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.cpu().numpy(), ref)
+    text = terminal.ansi_halfblocks(ref)
+    assert text.count("\n") == 11 and text.count("▀") == 40 * 12

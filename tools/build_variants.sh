@@ -8,7 +8,7 @@ while [ $# -ge 2 ]; do
   NAME=$1; FLAGS=$2; shift 2
   OUT=build/variants/$NAME; mkdir -p $OUT
   pids=()
-  for f in tray_kernel.hip tray_abi.hip; do
+  for f in tray_kernel.hip tray_abi.hip tray_scale.hip; do
     /opt/rocm/bin/hipcc $BASE $FLAGS -c -o $OUT/$f.o csrc/$f & pids+=($!)
   done
   for f in tray_host.cpp tray_bvh.cpp; do

@@ -41,7 +41,7 @@ def main(argv=None) -> int:
         png.save_png(a.save, img)
     if a.ansi:
         cols, rows = terminal.terminal_size()
-        print(terminal.ansi_halfblocks(terminal.scale_image(img, cols, rows * 2)))
+        print(terminal.ansi_halfblocks(terminal.scale_image(img, cols, rows * 2, a.s)))
     return 0
 
 

@@ -132,6 +132,8 @@ EXPORTS = (
     "tray_render_devices",
     "tray_render_devices_progress",
     "tray_release_cache",
+    "tray_scale_rgba",
+    "tray_scale_rgba_async",
     "tray_scene_upload",
     "tray_scene_release",
     "tray_scene_get_info",
@@ -198,6 +200,9 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.tray_render_devices_progress.argtypes = L.tray_render_devices.argtypes + [PROGRESS_FN, vp]
     if hasattr(L, "tray_release_cache"):
         L.tray_release_cache.argtypes = [i32]
+    if hasattr(L, "tray_scale_rgba"):
+        L.tray_scale_rgba.argtypes = [vp, i32, i32, vp, i32, i32, i32, i32]
+        L.tray_scale_rgba_async.argtypes = [vp, i32, i32, vp, i32, i32, i32, i32, vp]
     if hasattr(L, "tray_linear_to_srgba_async"):
         L.tray_linear_to_srgba_async.argtypes = [vp, ctypes.c_size_t, vp, i32, vp]
     L.tray_scene_upload.argtypes = [vp, i32, ctypes.POINTER(Background), i32, ctypes.POINTER(vp)]
@@ -314,6 +319,24 @@ def render_devices(spheres, background: Background, camera: CameraState, params:
         with _Progress(progress) as cb:
             check(lib().tray_render_devices_progress(*args, cb.fn, None))
     return out, seg
+
+
+SCALE_NEAREST, SCALE_BILINEAR = 0, 1  # tray_scale_filter
+
+
+def scale_rgba(src: np.ndarray, dw: int, dh: int, bilinear: bool, dst: np.ndarray | None = None,
+               device: int = 0) -> np.ndarray:
+    """tray_scale_rgba: x/image/draw BiLinear / NearestNeighbor .Scale of an [H, W, 4]
+    uint8 image onto dst (a fresh zero image by default, as main.go:123), on the device."""
+    a = np.ascontiguousarray(src, dtype=np.uint8)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError("src must be [H, W, 4] uint8")
+    out = np.zeros((dh, dw, 4), dtype=np.uint8) if dst is None else np.array(dst, dtype=np.uint8, copy=True)
+    if out.shape != (dh, dw, 4):
+        raise ValueError("dst must be [dh, dw, 4] uint8")
+    check(lib().tray_scale_rgba(a.ctypes.data, a.shape[1], a.shape[0], out.ctypes.data, dw, dh,
+                                SCALE_BILINEAR if bilinear else SCALE_NEAREST, device))
+    return out
 
 
 def release_cache(device: int = -1) -> None:

@@ -141,6 +141,11 @@ static int device_state(int32_t device, DeviceState** out) {
     return TRAY_OK;
 }
 
+int device_usable(int32_t device) {
+    DeviceState* st = nullptr;
+    return device_state(device, &st);
+}
+
 }  // namespace tray
 
 // A scene resident on one device. Renders of one scene handle share its work

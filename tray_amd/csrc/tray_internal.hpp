@@ -10,6 +10,10 @@ namespace tray {
 // Records `msg` as tray_last_error() for the calling thread and returns `code`.
 int fail(int code, const std::string& msg);
 
+// TRAY_OK when `device` is a visible gfx950 device (first use: its one-time
+// setup, tray_abi.hip), else the tray_status and tray_last_error().
+int device_usable(int32_t device);
+
 // ColorF.ToSRGBA's channel encoder on the host (ray/vec3.go:173-180).
 uint8_t srgb8(double c);
 // The device encoder's table (tray_host.cpp): t[k], k = 1..255, is the smallest

@@ -1,14 +1,14 @@
 """Terminal sink of the reference's interactive binary (main.go:86-131): render at
-`supersample` x the terminal's cell grid (two pixel rows per text row), scale
-down bilinearly, draw with upper-half-block characters in 24-bit colour.
+`supersample` x the terminal's cell grid (two pixel rows per text row), scale to
+the terminal with golang.org/x/image/draw's scalers (BiLinear when
+supersampling, NearestNeighbor below 1, none at 1: main.go:119-128), draw with
+upper-half-block characters in 24-bit colour.
 
-Host code, not on the hot path. Parity unpinned: the
-scaler restates the published algorithm of golang.org/x/image/draw's
-`BiLinear.Scale` (a separable triangle-kernel filter whose support widens by
-the downscale factor, weights normalised per output pixel) and the drawing
-restates fortio.org/terminal/ansipixels' half-block output; neither library is
-present in the reference tree, and the reference's tests hold no fixture for
-either, so only the properties in tests/test_terminal_cpu.py are checked.
+Not on the hot path. The scaling runs on the device
+(tray_scale_rgba, tray_amd/csrc/tray_scale.hip), byte-identical to the oracle's
+restatement of the draw package's published algorithm; parity with the Go
+library itself is unpinned (golang.org/x/image and fortio.org/terminal are not
+vendored, and the reference holds no fixture of either).
 """
 from __future__ import annotations
 
@@ -17,47 +17,24 @@ import os
 
 import numpy as np
 
-
-def _weights(dw: int, sw: int, nearest: bool) -> np.ndarray:
-    """[dw, sw] contribution matrix, rows normalised (x/image/draw newDistrib:
-    center = (x + 0.5)·scale − 0.5, support 1 widened to `scale` when shrinking)."""
-    scale = sw / dw
-    w = np.zeros((dw, sw), dtype=np.float64)
-    if nearest:  # NearestNeighbor.Scale: source pixel floor((x + 0.5)·scale)
-        w[np.arange(dw), np.minimum(((np.arange(dw) + 0.5) * scale).astype(np.int64), sw - 1)] = 1.0
-        return w
-    half, arg_scale = 1.0, 1.0
-    if scale > 1:
-        half, arg_scale = scale, 1.0 / scale
-    for x in range(dw):
-        center = (x + 0.5) * scale - 0.5
-        i = max(0, math.floor(center - half))
-        j = min(sw, math.ceil(center + half))
-        if j < i:
-            j = i
-        ks = np.arange(i, j)
-        r = 1.0 - np.abs((center - ks) * arg_scale)  # triangle kernel, zero outside |t| < 1
-        r = np.where(r > 0, r, 0.0)
-        tot = r.sum()
-        if tot > 0:
-            w[x, i:j] = r / tot
-        else:  # no tap inside the support: nearest source pixel
-            w[x, min(sw - 1, max(0, math.floor(center + 0.5)))] = 1.0
-    return w
+from . import _lib
 
 
-def scale_image(img: np.ndarray, dw: int, dh: int) -> np.ndarray:
-    """Scale an [H, W, 4] uint8 RGBA image to [dh, dw, 4]: bilinear when
-    shrinking or equal (main.go:124-126 BiLinear), nearest when growing (:122)."""
-    sh, sw = img.shape[:2]
-    if (sh, sw) == (dh, dw):
+def scale_filter(supersample: float):
+    """main.go:121-128: the scaler for a supersampling factor ('bilinear',
+    'nearest', or None when the image already has the terminal's size)."""
+    if supersample == 1:
+        return None
+    return "nearest" if supersample < 1 else "bilinear"
+
+
+def scale_image(img: np.ndarray, dw: int, dh: int, supersample: float, device: int = 0) -> np.ndarray:
+    """The [H, W, 4] uint8 RGBA render scaled to [dh, dw, 4] as main.go:119-128
+    does: into a fresh image with draw.Over, on the device."""
+    f = scale_filter(supersample)
+    if f is None:
         return img.copy()
-    nearest = dw > sw or dh > sh
-    wx, wy = _weights(dw, sw, nearest), _weights(dh, sh, nearest)
-    src = img.astype(np.float64) * 257.0  # 16-bit channels, as image/color's RGBA()
-    tmp = np.einsum("xs,hsc->hxc", wx, src)
-    out = np.einsum("ys,sxc->yxc", wy, tmp)
-    return (np.clip(np.floor(out + 0.5), 0, 65535).astype(np.uint32) >> 8).astype(np.uint8)
+    return _lib.scale_rgba(img, dw, dh, bilinear=f == "bilinear", device=device)
 
 
 def ansi_halfblocks(img: np.ndarray) -> str:
