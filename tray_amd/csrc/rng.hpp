@@ -145,9 +145,16 @@ __host__ __device__ __forceinline__ void sincos_2pi_word(uint32_t w, double& s, 
     const double sd = sn, cd = cs;
     const double k = 1.5 - 0.5 * (sd * sd + cd * cd);
     const double sk = sd * k, ck = cd * k;
+    // Quadrant rotation (sincos_2pi's qq == 0: (sk, ck), 1: (ck, -sk), 2: (-sk, -ck),
+    // 3: (-ck, sk)) as one swap on bit 0 and sign flips on the high words: s is
+    // negated in quadrants 2 and 3, c in 1 and 2. Negation is exact, so the bits
+    // are those of the selects it replaces.
     const uint32_t qq = w >> 30;
-    s = qq == 0 ? sk : qq == 1 ? ck : qq == 2 ? -sk : -ck;
-    c = qq == 0 ? ck : qq == 1 ? -sk : qq == 2 ? -ck : sk;
+    const bool swap_sc = (qq & 1u) != 0u;
+    const double s0 = swap_sc ? ck : sk, c0 = swap_sc ? sk : ck;
+    const uint64_t sflip = (uint64_t)(qq >> 1) << 63, cflip = (uint64_t)((qq ^ (qq >> 1)) & 1u) << 63;
+    s = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, s0) ^ sflip);
+    c = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, c0) ^ cflip);
 }
 
 }  // namespace tray

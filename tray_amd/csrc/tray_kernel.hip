@@ -51,6 +51,14 @@ __device__ __forceinline__ D3 smul(D3 v, double t) { return d3(v.x * t, v.y * t,
 __device__ __forceinline__ D3 mul(D3 u, D3 v) { return d3(u.x * v.x, u.y * v.y, u.z * v.z); }
 __device__ __forceinline__ D3 sdiv(D3 v, double t) { return d3(v.x / t, v.y / t, v.z / t); }
 __device__ __forceinline__ D3 neg(D3 v) { return d3(-v.x, -v.y, -v.z); }
+// cond ? neg(v) : v as sign-bit flips (one mask, three XORs instead of six selects).
+__device__ __forceinline__ double flip(double x, uint64_t m) {
+    return __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, x) ^ m);
+}
+__device__ __forceinline__ D3 neg_if(D3 v, bool cond) {
+    const uint64_t m = (uint64_t)cond << 63;
+    return d3(flip(v.x, m), flip(v.y, m), flip(v.z, m));
+}
 
 // a / b, correctly rounded, given y = RN(1/b) (exactly rounded, e.g. a full
 // division or a host-side 1.0/b): q = RN(a*y) is within 1 ulp of a/b, the
@@ -828,7 +836,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
         const D3 point = add(L.org, smul(L.dir, closest));                             // Ray.At (ray/ray.go:23-25)
         const D3 outward = sdiv_rcp(sub(point, d3(g.x, g.y, g.z)), m.radius, m.rinv);  // ray/objects.go:100
         const bool front = dot(L.dir, outward) < 0;                                    // SetFaceNormal (:19-26)
-        const D3 normal = front ? outward : neg(outward);
+        const D3 normal = neg_if(outward, !front);
         bool scattered = true;
         D3 new_dir;
         D3 att = d3(m.albedo[0], m.albedo[1], m.albedo[2]);
@@ -867,7 +875,12 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     // Settle the shading-record loads here, on every path: vmcnt is one in-order
     // counter, so a load still pending when end_path stores would make the next
     // write of its registers wait for the stores' write-back too.
+#ifndef TRAY_SHADE_SETTLE
+#define TRAY_SHADE_SETTLE 1
+#endif
+#if TRAY_SHADE_SETTLE
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
     if (!ends) return true;
     end_path<kStats>(p, L, color, st);
     return false;
