@@ -36,10 +36,12 @@ __device__ __forceinline__ double sqrt_core(double x) {
 __device__ __forceinline__ uint32_t hi_word(double x) { return (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32); }
 // x in [2^-767, 2^1024): biased exponent 256..2046, sign clear.
 __device__ __forceinline__ bool sqrt_core_ok(double x) { return hi_word(x) - 0x10000000u < 0x6FF00000u; }
+// Zeros also take the full lowering (it returns x for +-0): they are rare on
+// every path that calls this (a tangent ray's discriminant, a Philox word of
+// 0, normal incidence), so the common path carries no zero test and select.
 __device__ __forceinline__ double sqrt_cr(double x) {
     double g = sqrt_core(x);
-    if (x == 0) g = x;
-    if (__builtin_expect(!((x == 0) | sqrt_core_ok(x)), 0)) g = __builtin_sqrt(x);
+    if (__builtin_expect(!sqrt_core_ok(x), 0)) g = __builtin_sqrt(x);
     return g;
 }
 __device__ __forceinline__ double rcp_core(double b) {

@@ -96,7 +96,8 @@ __device__ __forceinline__ double div_root(double a, double b, double y) {
     const double q = a * y;
     const double r = __builtin_fma(-b, q, a);
     const double q1 = __builtin_fma(r, y, q);
-    if (__builtin_expect((hi_word(q) & 0x7FF00000u) >= (1983u << 20), 0)) return a / b;
+    // biased exponent >= 1983 (one 32-bit field extract and compare)
+    if (__builtin_expect(__builtin_amdgcn_ubfe(hi_word(q), 20u, 11u) >= 1983u, 0)) return a / b;
     return q1;
 }
 __device__ __forceinline__ double dot(D3 u, D3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
@@ -455,10 +456,13 @@ __device__ __forceinline__ void test_geo(Trav& T, const SceneView& sv, const dou
         const double sq = sqrt_cr(d);
         const double r1 = div_root(h - sq, T.a, T.a_inv);
         const double t = r1 > 1e-6 ? r1 : div_root(h + sq, T.a, T.a_inv);
-        if (t > 1e-6 && (t < T.closest || (t == T.closest && T.slot >= 0 && sv.bidx[slot] < sv.bidx[T.slot]))) {
-            T.closest = t;
-            T.slot = slot;
-        }
+        // Accept with selects; only an exact tie with an earlier hit branches (to read
+        // both list indices).
+        const bool front = t > 1e-6;
+        bool take = front & (t < T.closest);
+        if (__builtin_expect(front & (t == T.closest) & (T.slot >= 0), 0)) take = sv.bidx[slot] < sv.bidx[T.slot];
+        T.closest = take ? t : T.closest;
+        T.slot = take ? slot : T.slot;
     }
 }
 __device__ __forceinline__ void test_slot(Trav& T, const SceneView& sv, int32_t slot, const D3& org, const D3& dir) {
