@@ -202,6 +202,8 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--markdown", action="store_true")
     ap.add_argument("--layout", type=int, default=1, help="LDS layout instance (1: book cover; 2: dense C5)")
+    ap.add_argument("--list", default=None, metavar="PHASE",
+                    help="print the hot instructions of one phase (address, instruction, innermost function:line)")
     args = ap.parse_args()
     global KERNEL
     KERNEL = KERNEL.replace("ILi1E", f"ILi{args.layout}E")
@@ -239,6 +241,8 @@ def main():
         hot = block[k] not in cold_blocks
         u = unit_of(i["mn"])
         key = ph if hot else ph + ":cold"
+        if args.list == key:
+            print(f"{i['addr']:6x}  {i['mn']:<24} {i['ops'][:48]:<48} {st[0][0][:40]}:{st[0][1]}")
         static[key]["inst"] += 1
         static[key]["unit:" + u] += 1
         if u == "valu":
@@ -295,6 +299,8 @@ def main():
         rec["dynamic_estimate"] = est
 
     js = json.dumps(rec, indent=1)
+    if args.list:
+        return
     if args.json:
         open(args.json, "w").write(js + "\n")
     if args.markdown:
