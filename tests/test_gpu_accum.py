@@ -1,0 +1,124 @@
+"""Fixed-point accumulation of a pixel's samples ("Accumulation").
+
+Frames whose rays_per_pixel is a multiple of 64 (every benchmark config but C1)
+sum each pixel's samples exactly as integers (the colour scaled by 2^k and
+rounded, k >= 44, so the mean is within 2^-45 of the exact mean of the FP64
+sample colours), on chip per 64-sample chunk when the LDS has room, else
+through the per-sample buffer. Both mechanisms give the same bits, whatever the
+order the samples finish in; against the oracle (Go's FP64 sum in sample order)
+the frames stay inside the parity bar of tests/test_gpu_parity.py (paths
+bit-exact, colour within 1e-12). Other frames keep the FP64 sum in sample order.
+The switches (TRAY_ACC_SLOTS, TRAY_FIXED_POINT) are read at every launch."""
+import contextlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import DEFAULT_BG, RICH_SETUP
+from test_gpu_parity import WORKERS, bg_struct, camera, check, gpu_render
+
+pytestmark = pytest.mark.gpu
+
+FIXED_TOL = 2.0 ** -44  # fixed point vs the FP64 sum of the same samples: 2^-45 + the FP64 sum's own rounding
+
+
+@contextlib.contextmanager
+def env(**kv):
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update({k: str(v) for k, v in kv.items()})
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+# width/height not multiples of 8: padding pixels in the last tiles (chunks that start no sample)
+@pytest.mark.parametrize("scene,spp", [("rich2", 64), ("rich2", 128), ("dense7", 64)])
+def test_on_chip_equals_sample_buffer_and_oracle(L, O, scene, spp):
+    sc = O.rich_scene(2) if scene == "rich2" else O.rich_scene(7, 22)
+    w, h = 37, 21
+    st = camera(L, RICH_SETUP, w, h)
+    base, bseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 5)
+    # per-sample buffer with integer resolve; one and two slots per wave (lanes wait for a free slot)
+    for slots in (0, 1, 2, 9):
+        with env(TRAY_ACC_SLOTS=slots):
+            rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 5)
+        assert np.array_equal(seg, bseg), slots
+        assert np.array_equal(rgb, base), slots
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, spp, 50, 0.5, 5, workers=WORKERS)
+    check(base, bseg, ref, rseg)
+
+
+def test_fixed_point_vs_fp64_sum(L, O):
+    sc = O.rich_scene(2)
+    w, h = 48, 27
+    st = camera(L, RICH_SETUP, w, h)
+    fixed, fseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 6)
+    with env(TRAY_FIXED_POINT=0):
+        f64, dseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 6)
+    assert np.array_equal(fseg, dseg)
+    err = float(np.max(np.abs(fixed - f64)))
+    assert err <= FIXED_TOL, err
+    assert not np.array_equal(fixed, f64)  # the two sums do differ in the last bits somewhere
+
+
+def test_fixed_point_formats_and_linear_scan(L, O):
+    sc = O.rich_scene(2)
+    w, h = 40, 22
+    st = camera(L, RICH_SETUP, w, h)
+    f64, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3)
+    f32, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3, output=L.OUT_RGB_F32)
+    assert np.array_equal(f32, f64.astype(np.float32))
+    u8, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3, output=L.OUT_RGBA8)
+    assert np.array_equal(u8, O.to_srgba(f64))
+    # the linear-scan kernel sums through the per-sample buffer: same bits
+    lin, lseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3, flags=L.FLAG_LINEAR_SCAN)
+    assert np.array_equal(lseg, seg) and np.array_equal(lin, f64)
+
+
+def test_bound_too_large_keeps_fp64_sum(L, O):
+    """Albedo 3 at depth 50 bounds the colour at 3^50: no usable scale, so the
+    frame is the FP64 sum in sample order (identical to TRAY_FIXED_POINT=0)."""
+    sc = O.rich_scene(2).copy()
+    lam = sc["material"] == 1
+    sc["albedo"][lam] *= 3.0
+    w, h = 24, 14
+    st = camera(L, RICH_SETUP, w, h)
+    a, sa = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 2)
+    with env(TRAY_FIXED_POINT=0):
+        b, sb = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 2)
+    assert np.array_equal(sa, sb) and np.array_equal(a, b)
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, 64, 50, 0.5, 2, workers=WORKERS)
+    assert np.array_equal(sa, rseg)
+    assert float(np.max(np.abs(a - ref))) <= 1e-12 * max(1.0, float(np.max(np.abs(ref))))
+
+
+def test_passes_and_tiles_with_chunk_partials(L, O):
+    """Several progressive passes in one launch (partials of every pass in one
+    buffer), row tiles, and a short launch band: bit-identical to single renders."""
+    import torch
+
+    from test_gpu_parity import _passes
+
+    sc = O.rich_scene(2)
+    w, h, spp = 40, 19, 128
+    st = camera(L, RICH_SETUP, w, h)
+    dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
+    try:
+        for band in (None, str(40 * 8 * spp * 3 * 2)):
+            with env(**({"TRAY_BAND_SAMPLES": band} if band else {})):
+                for tiles in [{}, dict(tile_rows=2, tile_count=3, tile_index=1)]:
+                    p = L.make_params(w, h, 50, spp, 0.5, 4, pass_=1, **tiles)
+                    rows = L.params_rows(p)
+                    frames = _passes(L, dev, st, p, 3, torch.float64, (rows, w, 3))
+                    for k in range(3):
+                        q = L.make_params(w, h, 50, spp, 0.5, 4, pass_=1 + k, **tiles)
+                        one, _ = L.render(sc, bg_struct(L, DEFAULT_BG), st, q, 0)
+                        assert np.array_equal(frames[k], one), (band, tiles, k)
+    finally:
+        dev.release()

@@ -166,6 +166,7 @@ struct tray_scene_s {
     tray::MatRec* mat;
     uint32_t* queue;
     tray::V3 bg_a, bg_b;
+    double max_att;  // max(1, |albedo| of every Lambertian/Metal sphere): bounds a path's throughput
     // exact-culling BVH (absent for tiny or non-finite scenes)
     bool has_bvh;
     double bvh_bound;
@@ -361,6 +362,13 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->geo = nullptr;
     sc->mat = nullptr;
     sc->queue = nullptr;
+    sc->max_att = 1.0;
+    for (int32_t i = 0; i < n; ++i)
+        if (spheres[i].material != TRAY_DIELECTRIC)  // Dielectric attenuates by exactly 1
+            for (int c = 0; c < 3; ++c) {
+                const double a = std::fabs(spheres[i].albedo[c]);
+                sc->max_att = a > sc->max_att || a != a ? (a != a ? HUGE_VAL : a) : sc->max_att;
+            }
     sc->bg_a = V3{bg->color_a[0], bg->color_a[1], bg->color_a[2]};
     sc->bg_b = V3{bg->color_b[0], bg->color_b[1], bg->color_b[2]};
     // One arena, filled from one host image with one copy: eleven allocations
@@ -449,6 +457,34 @@ static bool cand_enabled() {
     return !(e && *e && atoi(e) == 0);
 }
 
+// The fixed-point scale 2^k of a render (tray_kernel.hpp), or 0 for the FP64
+// sum in sample order. Fixed point needs 64 | rays_per_pixel (a 64-item chunk is
+// then one pixel's samples) and a colour bound that leaves k >= kAccMinShift:
+// a sample's colour is its throughput (a product of <= max_depth attenuations,
+// each <= max_att) times a convex combination of the two background colours,
+// so |c| <= C = max|bg| * max_att^max_depth (x 1.001 for rounding). k is the
+// largest shift with C * 2^k <= 2^kAccBits (tray_kernel.hpp).
+// TRAY_FIXED_POINT=0 forces the FP64 sum (tests, A/B).
+static int32_t fixed_point_shift(const tray_scene_s* sc, const tray_params* p) {
+    if (p->rays_per_pixel % 64 != 0) return 0;
+    if (const char* e = getenv("TRAY_FIXED_POINT"))
+        if (*e && atoi(e) == 0) return 0;
+    double bg = 0.0;
+    const double comps[6] = {sc->bg_a.x, sc->bg_a.y, sc->bg_a.z, sc->bg_b.x, sc->bg_b.y, sc->bg_b.z};
+    for (double c : comps) {
+        if (!std::isfinite(c)) return 0;
+        bg = std::max(bg, std::fabs(c));
+    }
+    if (!std::isfinite(sc->max_att)) return 0;
+    const double bound = bg * std::pow(sc->max_att, (double)p->max_depth) * 1.001;
+    if (!(bound < 0x1p20)) return 0;
+    int e = 0;
+    std::frexp(std::max(bound, 0x1p-300), &e);  // bound < 2^e
+    if (p->rays_per_pixel > (1 << 15)) return 0;  // the pixel's total r x 2^47 must stay below 2^63
+    const int32_t k = kAccBits - e;
+    return k >= kAccMinShift ? std::min(k, 600) : 0;
+}
+
 static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
                              uint32_t* segments_device, unsigned long long* stats_device, void* stream,
                              int32_t n_passes = 1, unsigned long long* progress_device = nullptr) {
@@ -487,6 +523,14 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.cam.aperture = cam->aperture;
     k.bg_a = sc->bg_a;
     k.bg_b = sc->bg_b;
+    k.acc_shift = fixed_point_shift(sc, p);
+    if (k.acc_shift > 0) {  // the scale rides on the background: every colour is then scaled (exactly)
+        for (V3* v : {&k.bg_a, &k.bg_b}) {
+            v->x = std::ldexp(v->x, k.acc_shift);
+            v->y = std::ldexp(v->y, k.acc_shift);
+            v->z = std::ldexp(v->z, k.acc_shift);
+        }
+    }
     k.out = out_device;
     k.passes = (uint32_t)n_passes;
     k.pass0 = (uint32_t)p->pass;
@@ -518,7 +562,7 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     const uint64_t spp_launch = (uint64_t)p->rays_per_pixel * (uint64_t)n_passes;
     if (!band_fits(p->width, spp_launch))
         return fail(TRAY_ERR_TOO_LARGE, "width x rays_per_pixel x passes too large (8 rows of samples exceed 2^31)");
-    const size_t need = sample_buffer_bytes(p->width, k.rows, spp_launch);
+    const size_t need = accum_buffer_bytes(p->width, k.rows, spp_launch, launch_layout(k, use_bvh).acc_slots > 0);
     if (need > sc->samples_bytes) {
         if (sc->samples) {
             TRAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));

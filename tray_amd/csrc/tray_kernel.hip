@@ -255,7 +255,24 @@ struct Lane {
     uint32_t item;                              // work item (sample) index in the band
     uint32_t pixel, sample, bounce, segments;  // segments of this path
     int32_t x, j;                               // image column, compact output row
+    uint32_t slot;                              // on-chip accumulation: the wave's slot of this sample's chunk
     bool busy;
+};
+
+// On-chip accumulation (kAcc; rays per pixel a multiple of 64, so a 64-item
+// chunk is 64 samples of one pixel and one wave takes all of them): the wave
+// keeps kAccCopies sets of three sums per open chunk (a slot) in LDS. A
+// finishing sample adds its rounded, scaled colour there with non-returning
+// LDS atomics (lanes of one wave may finish samples of one chunk in the same
+// instruction; lane l adds to set l % kAccCopies, which halves the same-address
+// serialisation); the adds are exact, so their order does not matter. Slots
+// are retired lazily (acc_retire): when the wave needs a slot and has none
+// free, every open chunk that no busy lane still traces writes its sums to
+// global memory (one 32-B record per 64 samples instead of 24 B per sample)
+// and is freed; at exit the wave retires the rest. No per-sample bookkeeping.
+typedef __attribute__((address_space(3))) double LdsF64;
+struct AccCtx {
+    LdsF64* slabs;  // this wave's slots: kAccCopies x 3 sums each
 };
 
 
@@ -756,12 +773,24 @@ __device__ __forceinline__ void start_sample(const KernelParams& p, UniPtr uni, 
 // A path ended with `color`: store it in the band's sample buffer (the resolve
 // kernel adds a pixel's samples in sample order, Add(colorSum, color) of
 // ray/tracer.go:143), count its segments, free the lane.
-template <bool kStats>
-__device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st) {
-    double* o = p.samples + (size_t)L.item * 3;
-    o[0] = color.x;
-    o[1] = color.y;
-    o[2] = color.z;
+// With kAcc the colour goes to the chunk's LDS accumulator instead (above):
+// the colour is already scaled by 2^acc_shift (through the background) and is
+// rounded to an integer (tray_kernel.hpp), added with a non-returning LDS
+// atomic (exact, so in any order).
+template <bool kStats, bool kAcc>
+__device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st,
+                                         const AccCtx& acc) {
+    if constexpr (kAcc) {
+        LdsF64* s = acc.slabs + (L.slot * kAccCopies + (threadIdx.x % kAccCopies)) * 3u;
+        __hip_atomic_fetch_add(s + 0, __builtin_rint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(s + 1, __builtin_rint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(s + 2, __builtin_rint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    } else {
+        double* o = p.samples + (size_t)L.item * 3;
+        o[0] = color.x;
+        o[1] = color.y;
+        o[2] = color.z;
+    }
     if (p.segments) atomicAdd(p.segments + (size_t)L.j * (size_t)p.width + (size_t)L.x, L.segments);
     if constexpr (kStats) st.segments += L.segments;
     L.busy = false;
@@ -797,6 +826,40 @@ __device__ __forceinline__ void count_progress(const KernelParams& p, bool ended
     }
 }
 
+// kAcc, wave-uniform: retire every open chunk (a slot in `open`) that no busy
+// lane still traces: its 64 samples have all been added, so its partial sums
+// go to global memory (record `chunk` of the launch band, kept per slot in
+// `chunk_of`: lane s holds slot s's chunk), its slot is zeroed and freed.
+// Called only when the wave finds no free slot, and at exit: the busy lanes'
+// slots are found by one ballot per open slot. A wave's LDS operations complete
+// in issue order, so the reads see every addition its lanes made.
+__device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccCtx& acc, uint64_t open, bool busy,
+                                               uint32_t slot, uint32_t chunk_of, uint32_t lane) {
+    uint64_t freed = 0;
+    while (open != 0ull) {
+        const uint32_t s0 = (uint32_t)__builtin_ctzll(open);
+        open &= open - 1ull;
+        if (__ballot(busy && slot == s0) != 0ull) continue;
+        volatile LdsF64* v = acc.slabs + s0 * kAccCopies * 3u;
+        double sum[3] = {0.0, 0.0, 0.0};  // integers below 2^53: exact in any order
+#pragma unroll
+        for (int k = 0; k < kAccCopies; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) sum[c] += v[3 * k + c];
+        if (lane == 0u) {
+            const uint32_t chunk = __builtin_amdgcn_readlane(chunk_of, s0);
+            AccPartial* o = reinterpret_cast<AccPartial*>(p.samples) + chunk;
+            o->sum[0] = sum[0];
+            o->sum[1] = sum[1];
+            o->sum[2] = sum[2];
+#pragma unroll
+            for (int k = 0; k < 3 * kAccCopies; ++k) v[k] = 0.0;
+        }
+        freed |= 1ull << s0;
+    }
+    return freed;
+}
+
 // One recursion level of RayColor (ray/objects.go:49-62) after Scene.Hit gave
 // (best, closest): the sky on a miss, else the hit record and the material's
 // scatter. `geo_at`/`mat_at` give the hit sphere's geometry and shading record.
@@ -809,9 +872,9 @@ __device__ __forceinline__ void count_progress(const KernelParams& p, bool ended
 #ifndef TRAY_EARLY_MAT
 #define TRAY_EARLY_MAT 1
 #endif
-template <bool kStats, typename GeoAt, typename MatAt>
+template <bool kStats, bool kAcc, typename GeoAt, typename MatAt>
 __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
-                                           double dir_lsq, GeoAt geo_at, MatAt mat_at, Stats& st) {
+                                           double dir_lsq, GeoAt geo_at, MatAt mat_at, Stats& st, const AccCtx& acc) {
     const bool hit = best >= 0;
     // A hit at the last level ends the path black whatever its material does
     // (RayColor(depth 0) is black), so no scatter is computed for it.
@@ -886,7 +949,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #endif
     if (!ends) return true;
-    end_path<kStats>(p, L, color, st);
+    end_path<kStats, kAcc>(p, L, color, st, acc);
     return false;
 }
 
@@ -999,7 +1062,8 @@ __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (si
 // LDS with sphere geometry in global memory (scenes too big for 1; BVH only).
 // kProg: the live-progress instance (tray_render_progress only), so the other
 // instances carry no progress code or registers.
-template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg>
+// kAcc: on-chip fixed-point accumulation of each 64-sample chunk (end_path).
+template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg, bool kAcc>
 __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
     extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
     __attribute__((address_space(3))) Uniforms* uni_lds =
@@ -1072,6 +1136,18 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
         sv.geo = smem;
     }
+    // [acc: waves x acc_slots x kAccSlotBytes] at acc_off
+    AccCtx acc{nullptr};
+    uint64_t acc_free = 0;   // kAcc, wave-uniform: free slots
+    uint64_t acc_all = 0;    // kAcc, wave-uniform: every slot
+    uint32_t acc_chunk = 0;  // kAcc: lane s holds the chunk of slot s
+    if constexpr (kAcc) {
+        LdsF64* all = (LdsF64*)reinterpret_cast<double*>(reinterpret_cast<char*>(smem_all) + p.acc_off);
+        const uint32_t waves = blockDim.x / 64u, slots = (uint32_t)p.acc_slots;
+        for (uint32_t i = threadIdx.x; i < waves * slots * kAccCopies * 3u; i += blockDim.x) all[i] = 0.0;
+        acc.slabs = all + (threadIdx.x / 64u) * slots * kAccCopies * 3u;
+        acc_free = acc_all = slots >= 64u ? ~0ull : (1ull << slots) - 1ull;
+    }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -1081,6 +1157,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     Trav T;
     T.cur = kBvhNone;  // idle
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
+    uint32_t pool_slot = 0;                 // kAcc, wave-uniform: the current chunk's accumulator slot
     bool exhausted = false;
 #ifdef TRAY_STATS_GROUND
     uint32_t gcls = 0;  // diagnostic: class of the lane's current segment (1/2: from an out-of-tree sphere, up / other)
@@ -1106,7 +1183,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         if (__popcll(idle) < TRAY_REFILL_BATCH && idle != ~0ull) idle = 0ull;  // batch refills
         // Items are assigned first (cheap, may span two chunks); the camera rays of
         // all newly assigned lanes are then generated together.
-        uint32_t fresh_item = ~0u;
+        uint32_t fresh_item = ~0u, fresh_slot = 0u;
         bool cam_hit = false;  // a camera ray whose Scene.Hit the candidate list answered in this refill
 #ifdef TRAY_PROFILE_CANDWAIT
         uint64_t prof_wait = 0;
@@ -1116,6 +1193,22 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #endif
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
+                if constexpr (kAcc) {
+                    // A chunk needs a free accumulator: with none, the idle lanes wait
+                    // for one of the wave's open chunks to finish (every open chunk
+                    // has a sample in flight, so one will).
+                    if (acc_free == 0ull) {
+                        // Retire the chunks no busy lane traces any more (lanes assigned in
+                        // this refill have not started yet: their chunk is open regardless).
+                        const bool held = L.busy || fresh_item != ~0u;
+                        acc_free = acc_retire(p, acc, acc_all, held, L.busy ? L.slot : fresh_slot, acc_chunk, lane);
+                    }
+                    if (acc_free == 0ull) {
+                        // unreachable with nothing in flight: no chunk would hold a slot
+                        if (__ballot(L.busy || fresh_item != ~0u) == 0ull) __builtin_trap();
+                        break;
+                    }
+                }
                 const uint32_t c = take_chunk(p, uni, lane);
                 if (c == kPoolDone) {
                     exhausted = true;
@@ -1123,12 +1216,25 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 }
                 pool_next = c * 64u;
                 pool_end = pool_next + 64u;
+                if constexpr (kAcc) {
+                    // Every item of a chunk is one pixel's (64 | r): valid or padding together.
+                    int32_t cx, cj;
+                    uint32_t cs, cp;
+                    if (pool_next < p.items && decode_item(p, pool_next, cx, cj, cs, cp)) {
+                        pool_slot = (uint32_t)__builtin_ctzll(acc_free);
+                        acc_free &= ~(1ull << pool_slot);
+                        acc_chunk = lane == pool_slot ? c : acc_chunk;
+                    }
+                }
             }
             const uint32_t n_idle = (uint32_t)__popcll(idle);
             const uint32_t take = min(n_idle, pool_end - pool_next);
             if ((idle >> lane) & 1ull) {
                 const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
-                if (rank < take) fresh_item = pool_next + rank;
+                if (rank < take) {
+                    fresh_item = pool_next + rank;
+                    fresh_slot = pool_slot;
+                }
             }
             pool_next += take;
             idle = __ballot(!L.busy && fresh_item == ~0u);
@@ -1156,6 +1262,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 if constexpr (kBVH)
                     if (p.cand) cand = p.cand[(size_t)j * (size_t)p.width + (size_t)x];
                 start_sample(p, uni, L, fresh_item, x, j, (p.pass0 + pass) * (uint32_t)p.spp + smp);
+                L.slot = fresh_slot;
 #ifdef TRAY_PROFILE_REFILL
                 prof_cam = __builtin_amdgcn_s_memtime();
 #endif
@@ -1211,8 +1318,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 TRAY_MARK("refill_shade")
                 bool ended = false;
                 if (cam_hit) {
-                    if (shade_step<kStats>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
-                                           [&] { return sv.bmat[max(T.slot, 0)]; }, st)) {
+                    if (shade_step<kStats, kAcc>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
+                                                 [&] { return sv.bmat[max(T.slot, 0)]; }, st, acc)) {
                         ++L.segments;
                         trav_begin(T, sv, L.org, L.dir);
                         if constexpr (kStats) st.spheres += (uint64_t)sv.n_global;
@@ -1267,8 +1374,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 ++L.segments;
                 double closest;
                 const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
-                ended = !shade_step<kStats>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[max(best, 0)]; },  // NaN-padded: entry 0 exists
-                                            [&] { return best >= 0 ? p.mat[best] : MatRec{}; }, st);
+                ended = !shade_step<kStats, kAcc>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[max(best, 0)]; },  // NaN-padded: entry 0 exists
+                                                  [&] { return best >= 0 ? p.mat[best] : MatRec{}; }, st, acc);
             }
             if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
         } else {
@@ -1362,8 +1469,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #ifdef TRAY_PROBE_SHADE64
                     TRAY_PROBE_F64(TRAY_PROBE_SHADE64)
 #endif
-                    if (shade_step<kStats>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
-                                           [&] { return sv.bmat[max(T.slot, 0)]; }, st)) {
+                    if (shade_step<kStats, kAcc>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
+                                                 [&] { return sv.bmat[max(T.slot, 0)]; }, st, acc)) {
                         ++L.segments;
 #if defined(TRAY_STATS_GROUND) && !defined(TRAY_PROFILE)
                         {
@@ -1389,6 +1496,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         }
     }
     if constexpr (kProg) flush_progress(p, prog_cur, prog_cnt, lane);
+    if constexpr (kAcc) (void)acc_retire(p, acc, acc_all & ~acc_free, false, 0u, acc_chunk, lane);  // every lane is idle
     if constexpr (kStats) {
         atomicAdd(p.stats + 0, (unsigned long long)st.segments);
         atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
@@ -1433,12 +1541,10 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 // (the megakernel has finished with it), so no memset launch sits between
 // consecutive frames.
 // blockIdx.y is the pass within the launch.
-// The mean of a pixel's samples written in the output format (pixel `off` of pass `pass`).
+// A pixel's mean written in the output format (compact pixel (x, j) of pass `pass`).
 template <int kFmt>
-__device__ __forceinline__ void write_mean(const KernelParams& p, const double* srgb, D3 sum, int32_t x, int32_t j,
-                                           uint32_t pass) {
-    const double inv = 1.0 / (double)p.spp;  // colorSumDiv (ray/tracer.go:123)
-    const D3 mean = smul(sum, inv);
+__device__ __forceinline__ void write_pixel(const KernelParams& p, const double* srgb, D3 mean, int32_t x, int32_t j,
+                                            uint32_t pass) {
     const size_t off = (size_t)j * (size_t)p.width + (size_t)x;
     void* const out = static_cast<char*>(p.out) + (size_t)pass * p.out_frame_bytes;
     if constexpr (kFmt == kOutRGBF64) {
@@ -1455,6 +1561,34 @@ __device__ __forceinline__ void write_mean(const KernelParams& p, const double* 
         static_cast<uint32_t*>(out)[off] = srgba_word(srgb, mean.x, mean.y, mean.z);
     }
 }
+// The mean of a pixel's samples written in the output format (pixel `off` of pass `pass`).
+template <int kFmt>
+__device__ __forceinline__ void write_mean(const KernelParams& p, const double* srgb, D3 sum, int32_t x, int32_t j,
+                                           uint32_t pass) {
+    const double inv = 1.0 / (double)p.spp;  // colorSumDiv (ray/tracer.go:123)
+    const D3 mean = smul(sum, inv);
+    write_pixel<kFmt>(p, srgb, mean, x, j, pass);
+}
+
+// A pixel's fixed-point sums (tray_kernel.hpp): the exact integer total of its
+// r samples, converted to FP64 (one rounding) and scaled back by 2^-acc_shift
+// (exact); a channel with a NaN (non-finite) sample is NaN.
+template <int kFmt>
+__device__ __forceinline__ void write_acc_mean(const KernelParams& p, const double* srgb, const int64_t s[3],
+                                               uint32_t bad, int32_t x, int32_t j, uint32_t pass) {
+    const double unscale = __builtin_ldexp(1.0, -p.acc_shift);
+    D3 sum;
+    double* c = &sum.x;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[k] = (bad >> k) & 1u ? __builtin_nan("") : (double)s[k] * unscale;
+    write_mean<kFmt>(p, srgb, sum, x, j, pass);
+}
+// One rounded sample or chunk sum into a pixel's integer total; a non-finite
+// value (or, for a single sample, one beyond 2^kAccBits) flags the channel.
+__device__ __forceinline__ void acc_add(double v, double limit, int64_t& s, uint32_t& bad, int k) {
+    if (__builtin_fabs(v) <= limit) s += (int64_t)v;
+    else bad |= 1u << k;
+}
 
 // Staged resolve (rays per pixel a multiple of 8): a wave's 64 pixels are
 // consecutive work items, so their samples are one contiguous region of the
@@ -1464,8 +1598,13 @@ __device__ __forceinline__ void write_mean(const KernelParams& p, const double* 
 // lane adds its pixel's 8 samples from LDS in sample order.
 constexpr int kStageStride = 25;  // doubles per pixel slab in LDS: 24 + 1 of padding (bank spread)
 
-template <int kFmt, bool kStaged>
+// kMode: 0 FP64 sum in sample order, 1 the same staged through LDS (8 | r),
+// 2 fixed-point sums of the per-sample buffer, 3 fixed-point sums of the chunk
+// partials (on-chip accumulation, 64 | r).
+enum : int { kResolveF64 = 0, kResolveStaged = 1, kResolveFixed = 2, kResolvePartials = 3 };
+template <int kFmt, int kMode>
 __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
+    constexpr bool kStaged = kMode == kResolveStaged;
     __shared__ double srgb[256];
     if constexpr (kFmt == kOutRGBA8) {  // the encoder table, one entry per thread
         srgb[threadIdx.x] = p.srgb[threadIdx.x];
@@ -1480,7 +1619,27 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
     uint32_t s0, pass;
     const bool valid = decode_item(p, item0, x, j, s0, pass);
     D3 sum = d3(0, 0, 0);
-    if constexpr (kStaged) {
+    if constexpr (kMode == kResolvePartials) {
+        if (!valid) return;
+        const AccPartial* part = reinterpret_cast<const AccPartial*>(p.samples) + (item0 >> 6);
+        int64_t s[3] = {0, 0, 0};
+        uint32_t bad = 0u;
+        for (int32_t c = 0; c < p.spp / 64; ++c)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) acc_add(part[c].sum[k], 0x1p53, s[k], bad, k);
+        write_acc_mean<kFmt>(p, srgb, s, bad, x, j, pass);
+        return;
+    } else if constexpr (kMode == kResolveFixed) {
+        if (!valid) return;
+        const double* smp = p.samples + (size_t)item0 * 3;
+        int64_t s[3] = {0, 0, 0};
+        uint32_t bad = 0u;
+        for (int32_t k = 0; k < p.spp; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) acc_add(__builtin_rint(smp[3 * k + c]), 0x1p47, s[c], bad, c);
+        write_acc_mean<kFmt>(p, srgb, s, bad, x, j, pass);
+        return;
+    } else if constexpr (kStaged) {
         __shared__ double stage[4][64 * kStageStride];
         const uint32_t lane = threadIdx.x & 63u;
         double* st = stage[threadIdx.x >> 6];
@@ -1686,41 +1845,47 @@ hipError_t launch_to_srgba(const double* rgb, size_t n_pixels, uint32_t* rgba, c
 
 using KernelFn = void (*)(KernelParams);
 
-template <bool kBVH, bool kSpill, bool kStats, bool kProg>
+template <bool kBVH, bool kSpill, bool kStats, bool kProg, bool kAcc>
 static KernelFn pick_kernel3(int lds_mode) {
-    if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill, kProg>;
+    if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill, kProg, kAcc>;
     if constexpr (kBVH)
-        if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill, kProg>;
-    return render_kernel<0, kBVH, kStats, kSpill, kProg>;
+        if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill, kProg, kAcc>;
+    return render_kernel<0, kBVH, kStats, kSpill, kProg, kAcc>;
 }
 
 // Instrumentation: the stats instance counts segments and tests; the progress
 // instance feeds tray_render_progress; neither is ever timed by the bench.
-template <bool kBVH, bool kSpill>
+template <bool kBVH, bool kSpill, bool kAcc>
 static KernelFn pick_kernel2(int lds_mode, bool stats, bool progress) {
-    if (stats) return pick_kernel3<kBVH, kSpill, true, false>(lds_mode);
-    if (progress) return pick_kernel3<kBVH, kSpill, false, true>(lds_mode);
-    return pick_kernel3<kBVH, kSpill, false, false>(lds_mode);
+    if (stats) return pick_kernel3<kBVH, kSpill, true, false, kAcc>(lds_mode);
+    if (progress) return pick_kernel3<kBVH, kSpill, false, true, kAcc>(lds_mode);
+    return pick_kernel3<kBVH, kSpill, false, false, kAcc>(lds_mode);
 }
 
-static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, bool spill) {
-    if (!bvh) return pick_kernel2<false, false>(lds_mode, stats, progress);
-    return spill ? pick_kernel2<true, true>(lds_mode, stats, progress)
-                 : pick_kernel2<true, false>(lds_mode, stats, progress);
+// On-chip accumulation is built for the BVH kernel with the whole stack on
+// chip (launch_layout grants accumulators only then); every other launch sums
+// through the per-sample buffer.
+static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, bool spill, bool acc) {
+    if (!bvh) return pick_kernel2<false, false, false>(lds_mode, stats, progress);
+    if (spill) return pick_kernel2<true, true, false>(lds_mode, stats, progress);
+    return acc ? pick_kernel2<true, false, true>(lds_mode, stats, progress)
+               : pick_kernel2<true, false, false>(lds_mode, stats, progress);
 }
 
-template <bool kStaged>
+template <int kMode>
 static KernelFn pick_resolve2(int fmt) {
-    if (fmt == kOutRGBF64) return resolve_kernel<kOutRGBF64, kStaged>;
-    if (fmt == kOutRGBF32) return resolve_kernel<kOutRGBF32, kStaged>;
-    return resolve_kernel<kOutRGBA8, kStaged>;
+    if (fmt == kOutRGBF64) return resolve_kernel<kOutRGBF64, kMode>;
+    if (fmt == kOutRGBF32) return resolve_kernel<kOutRGBF32, kMode>;
+    return resolve_kernel<kOutRGBA8, kMode>;
 }
 
 // The staged resolve needs 8 | rays per pixel (whole 8-sample slabs).
-static KernelFn pick_resolve(int fmt, int32_t spp) {
-    bool staged = spp % 8 == 0;
+static KernelFn pick_resolve(const KernelParams& p) {
+    if (p.acc_shift > 0)
+        return p.acc_slots > 0 ? pick_resolve2<kResolvePartials>(p.out_format) : pick_resolve2<kResolveFixed>(p.out_format);
+    bool staged = p.spp % 8 == 0;
     if (const char* e = getenv("TRAY_RESOLVE_STAGED")) staged = staged && atoi(e) != 0;  // A/B
-    return staged ? pick_resolve2<true>(fmt) : pick_resolve2<false>(fmt);
+    return staged ? pick_resolve2<kResolveStaged>(p.out_format) : pick_resolve2<kResolveF64>(p.out_format);
 }
 
 // Blocks the device keeps resident for this kernel and LDS size (persistent grid cap).
@@ -1801,6 +1966,56 @@ size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp) {
     return (size_t)((width + 7) / 8) * 64u * (size_t)tile_rows * (size_t)spp * 3 * sizeof(double);
 }
 
+size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials) {
+    if (!partials) return sample_buffer_bytes(width, rows, spp);
+    if (rows <= 0) return 0;
+    const int32_t tile_rows = std::min(band_tile_rows(width, spp), (rows + 7) / 8);
+    return (size_t)((width + 7) / 8) * (size_t)tile_rows * (size_t)spp * sizeof(AccPartial);  // 64 x spp / 64
+}
+
+LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
+    LaunchLayout L{0, 0, 0, 0, 0};
+    if (use_bvh) {
+        // Whole scene in LDS when it fits next to kStackLdsMin stack slots, else
+        // the nodes and leaf table when they fit, else nothing; the stack then
+        // takes what LDS is left (up to its bound), the rest spills.
+        L.lds_mode = bvh_lds_plan(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap).mode;
+        if (const char* m = getenv("TRAY_BVH_LDS_MODE")) {  // tests / A-B: force a layout that fits
+            const int want = atoi(m);
+            if (want == 0 || (want == 2 && L.lds_mode != 0) ||
+                (want == 1 && bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap) <= kMaxLDSBytes))
+                L.lds_mode = want;
+        }
+        const size_t scene = L.lds_mode == 1   ? scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves)
+                             : L.lds_mode == 2 ? nodes_lds_bytes(p.n_nodes, p.n_leaves)
+                                               : 0;
+        const size_t room = kMaxLDSBytes - kUniformsBytes - scene;
+        L.stack_lds = std::min<int32_t>(p.stack_cap, (int32_t)(room / kStackSlotBytes));
+        if (const char* cap = getenv("TRAY_STACK_LDS_SLOTS"))  // tests: force the overflow path
+            L.stack_lds = std::min(L.stack_lds, std::max<int32_t>(kStackLdsMin, atoi(cap)));
+        L.lds = kUniformsBytes + bvh_stack_bytes(L.stack_lds) + scene;
+        // Chunk accumulators in what the whole stack leaves (fixed-point frames only).
+        if (p.acc_shift > 0 && L.stack_lds == p.stack_cap && p.spp % 64 == 0) {
+            const size_t waves = (size_t)kBvhBlock / 64u;
+            const size_t per_slot = waves * kAccSlotBytes;
+            const size_t left = kMaxLDSBytes - L.lds;
+            int32_t slots = (int32_t)std::min<size_t>(kAccSlotsMax, left / per_slot);
+            if (const char* e = getenv("TRAY_ACC_SLOTS"))  // tests / A-B: fewer slots, 0 = off
+                slots = std::min(slots, std::max(0, atoi(e)));
+            if (slots >= kAccSlotsMin || (slots > 0 && getenv("TRAY_ACC_SLOTS"))) {
+                L.acc_slots = slots;
+                L.acc_off = (uint32_t)L.lds;
+                L.lds += (size_t)slots * per_slot;
+            }
+        }
+    } else {
+        const size_t geo = (size_t)p.n_pad * sizeof(double4);
+        L.lds_mode = geo + kUniformsBytes <= kMaxLDSBytes ? 1 : 0;
+        L.lds = kUniformsBytes + (L.lds_mode ? geo : 0);
+    }
+    return L;
+}
+
 bool band_fits(int32_t width, uint64_t spp) {
     return (uint64_t)((width + 7) / 8) * 64u * spp <= 0x7FFFFFFFull;
 }
@@ -1818,37 +2033,19 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    int lds_mode;
-    size_t lds;
-    if (use_bvh) {
-        // Whole scene in LDS when it fits next to kStackLdsMin stack slots, else
-        // the nodes and leaf table when they fit, else nothing; the stack then
-        // takes what LDS is left (up to its bound), the rest spills.
-        lds_mode = bvh_lds_plan(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap).mode;
-        if (const char* m = getenv("TRAY_BVH_LDS_MODE")) {  // tests / A-B: force a layout that fits
-            const int want = atoi(m);
-            if (want == 0 || (want == 2 && lds_mode != 0) ||
-                (want == 1 && bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap) <= kMaxLDSBytes))
-                lds_mode = want;
-        }
-        const size_t scene = lds_mode == 1   ? scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves)
-                             : lds_mode == 2 ? nodes_lds_bytes(p.n_nodes, p.n_leaves)
-                                             : 0;
-        const size_t room = kMaxLDSBytes - kUniformsBytes - scene;
-        p.stack_lds = std::min<int32_t>(p.stack_cap, (int32_t)(room / kStackSlotBytes));
-        if (const char* cap = getenv("TRAY_STACK_LDS_SLOTS"))  // tests: force the overflow path
-            p.stack_lds = std::min(p.stack_lds, std::max<int32_t>(kStackLdsMin, atoi(cap)));
-        if (p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
-        lds = kUniformsBytes + bvh_stack_bytes(p.stack_lds) + scene;
-    } else {
-        const size_t geo = (size_t)p.n_pad * sizeof(double4);
-        lds_mode = geo + kUniformsBytes <= kMaxLDSBytes ? 1 : 0;
-        lds = kUniformsBytes + (lds_mode ? geo : 0);
-    }
+    if (p.acc_shift > 0 && p.spp % 64 != 0) return hipErrorInvalidValue;  // the caller decides (fixed_point_shift)
+    const LaunchLayout layout = launch_layout(p, use_bvh);
+    const int lds_mode = layout.lds_mode;
+    const size_t lds = layout.lds;
+    p.stack_lds = layout.stack_lds;
+    p.acc_slots = layout.acc_slots;
+    p.acc_off = layout.acc_off;
+    if (use_bvh && p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
-    const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr, use_bvh && p.stack_cap > p.stack_lds);
-    const KernelFn resolve = pick_resolve(p.out_format, p.spp);
+    const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr,
+                                    use_bvh && p.stack_cap > p.stack_lds, p.acc_slots > 0);
+    const KernelFn resolve = pick_resolve(p);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {
         int dev;

@@ -97,7 +97,14 @@ struct KernelParams {
     size_t out_frame_bytes;  // output stride between passes
     int32_t j0, band_rows;  // the band: compact rows [j0, j0 + band_rows)
     FastDiv div_spp, div_tiles_x, div_tile_rows;  // item decoding; compact row -> image row
-    double* samples;     // per-item path colours (3 doubles), summed in order by the resolve kernel
+    double* samples;     // per-item path colours (3 doubles), summed by the resolve kernel; with
+                         // on-chip accumulation (acc_slots > 0) the same buffer holds AccPartial records
+    // Fixed-point accumulation (acc_shift > 0, rays_per_pixel a multiple of 64):
+    // the background is pre-scaled by 2^acc_shift, each sample's scaled colour is rounded to
+    // an integer and the integers are summed exactly (order-free); 0: FP64 sum in sample order.
+    int32_t acc_shift;
+    int32_t acc_slots;   // >0: per-wave LDS accumulators (slots per wave), partial per 64-item chunk
+    uint32_t acc_off;    // byte offset of the accumulator region in the kernel's dynamic LDS
     const Bvh4Node* nodes;  // exact-culling 4-wide BVH (tray_bvh.cpp), root first
     const int32_t* leaves;  // per leaf: (first slot << 3) | count
     int32_t leaf_single;    // 1: every leaf holds one sphere and its index is its slot
@@ -126,6 +133,46 @@ struct KernelParams {
 };
 
 hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
+
+// Fixed-point accumulation. A sample's colour c (already scaled by 2^k through
+// the background) is rounded to the integer v = rint(c), |v| <= 2^kAccBits; any
+// sum of at most 64 such integers is itself an integer of magnitude <= 2^53, so
+// FP64 adds it exactly: a chunk's sum (64 samples of one pixel) does not depend
+// on the order in which its samples finish, and the resolve pass adds a pixel's
+// chunk sums as 64-bit integers. A NaN sample makes its channel's sum NaN.
+constexpr int32_t kAccBits = 47;
+// A frame whose colour bound leaves the scale 2^k below 2^kAccMinShift (the
+// absolute resolution of a sample, 2^-k) keeps the FP64 sum in sample order.
+constexpr int32_t kAccMinShift = 44;
+// One chunk's sums in global memory (exact integers held as doubles): 32 B.
+struct AccPartial {
+    double sum[3];
+    double pad;
+};
+static_assert(sizeof(AccPartial) == 32, "AccPartial layout");
+// In LDS each open chunk has TRAY_ACC_COPIES sets of three sums; lane l adds to
+// set l % copies, so fewer lanes of a wave hit one address in one instruction.
+#ifndef TRAY_ACC_COPIES
+#define TRAY_ACC_COPIES 2
+#endif
+constexpr int32_t kAccCopies = TRAY_ACC_COPIES;
+constexpr size_t kAccSlotBytes = (size_t)kAccCopies * 3 * sizeof(double);
+constexpr int32_t kAccSlotsMax = 64;  // per wave (the free-slot mask is 64 bits)
+constexpr int32_t kAccSlotsMin = 8;
+
+// Where a launch keeps things (launch_render; render_async_impl sizes its
+// buffers from it): the scene layout, stack slots in LDS, LDS bytes, and
+// whether the chunk accumulators fit next to them.
+struct LaunchLayout {
+    int lds_mode;
+    int32_t stack_lds;
+    size_t lds;
+    int32_t acc_slots;  // 0: accumulate through the per-sample buffer
+    uint32_t acc_off;
+};
+LaunchLayout launch_layout(const KernelParams& p, bool use_bvh);
+// Device bytes of the per-sample buffer or (acc_slots > 0) the chunk partials.
+size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials);
 
 // Primary-ray candidates: for every compact pixel of p's rows, the
 // tree spheres (leaf slots) that any camera ray of the pixel can reach, by a
