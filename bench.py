@@ -367,6 +367,8 @@ def main() -> int:
             "frames_per_launch": F,
         },
         "single_launch_ms": round(single_ms, 4) if single_ms else None,
+        "accumulation": "fixed-point chunk sums in LDS (exact, order-free; DESIGN.md 5)" if spp % 64 == 0
+                        else "FP64 sum in sample order",
     }
     if dist_rec:
         rec["rccl_world"] = dist_rec["world"] if backend == "nccl" else None
@@ -408,8 +410,10 @@ def main() -> int:
                          "peak = 78.6 TFLOP/s FP64 vector spec / 2 = 39.3 T ops/s",
             "algorithmic_bytes_per_launch": alg_bytes,
             "traffic_over_algorithmic": round(traffic / alg_bytes, 2) if traffic else None,
-            "traffic_note": "megakernel HBM bytes by PMC (FETCH_SIZE x2 + WRITE_SIZE): the 24-B colour per sample "
-                            "the resolve pass sums in sample order (DESIGN.md 5)",
+            "traffic_note": "megakernel HBM bytes by PMC (FETCH_SIZE x2 + WRITE_SIZE). With 64 | r each pixel's "
+                            "samples are summed exactly in LDS as fixed-point integers and the megakernel writes one "
+                            "32-B record per 64-sample chunk (DESIGN.md 5, Accumulation); the resolve pass turns them "
+                            "into the frames",
             "traversal": "linear scan" if args.linear else "exact-culling 4-wide BVH; camera rays: per-pixel "
                                                             "candidate lists (no traversal)",
             "ops_note": "achieved counts the work executed: the candidate lists removed ~35 % of the box tests "

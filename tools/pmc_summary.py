@@ -18,7 +18,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = ", true, false, false, false>"  # the timed BVH kernel, any LDS layout (1: book cover, 2: dense C5)
+KERNEL = ", true, false, false, false, true>"  # the timed BVH kernel (on-chip accumulation), any LDS layout (1: book cover, 2: dense C5)
 
 
 def values(path):
@@ -61,15 +61,17 @@ def main():
     rec = {
         "config": args.config,
         "frames_per_launch": args.frames,
-        "kernel": "tray::render_kernel<L, true, false, false, false> (BVH, LDS layout L, no stack spill)",
+        "kernel": "tray::render_kernel<L, true, false, false, false, true> (BVH, LDS layout L, no stack spill, on-chip accumulation)",
         "bands_per_launch": bands,
         "FETCH_SIZE_KB_raw_per_dispatch": fetch_kb,
         "WRITE_SIZE_KB_per_dispatch": write_kb,
         "fetch_bytes_corrected": fetch,
         "write_bytes": write,
         "hbm_bytes_per_launch": int(fetch + write),
-        "note": "megakernel only, per launch (frames_per_launch frames); its HBM traffic is the per-sample "
-                "colour buffer (24 B/sample). The resolve kernel reads it back.",
+        "note": "megakernel only, per launch (frames_per_launch frames). With on-chip accumulation (64 | r) it "
+                "writes one 32-B record of fixed-point sums per 64-sample chunk and reads the primary-ray "
+                "candidate records (16 B per pixel per frame); without it, one 24-B colour per sample. The "
+                "resolve kernel reads the records back and writes the frames.",
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md HBM "
                   "section: FETCH_SIZE x2 on gfx950, WRITE_SIZE exact); median over the warm dispatches x "
                   "bands_per_launch",
