@@ -265,6 +265,7 @@ def main() -> int:
     F = max(1, min(args.passes, args.steps))
     nslot = max(1, args.frames_in_flight)
     scenes = [_lib.DeviceScene(spheres, bg, local_rank) for _ in range(nslot)]
+    plan = scenes[0].plan(cam._state, params, F).as_dict()  # tray_render_plan_get: how the timed launches run
     outs = [torch.empty((F, rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslot - 1)]
     comm = torch.cuda.Stream() if world > 1 else None
@@ -367,8 +368,10 @@ def main() -> int:
             "frames_per_launch": F,
         },
         "single_launch_ms": round(single_ms, 4) if single_ms else None,
-        "accumulation": "fixed-point chunk sums in LDS (exact, order-free; DESIGN.md 5)" if spp % 64 == 0
-                        else "FP64 sum in sample order",
+        "accumulation": ("fixed-point chunk sums in LDS (exact, order-free; DESIGN.md 5)" if plan["acc_slots"] > 0
+                         else "fixed-point sums through the per-sample buffer" if plan["fixed_point_shift"] > 0
+                         else "FP64 sum in sample order"),
+        "plan": plan,
     }
     if dist_rec:
         rec["rccl_world"] = dist_rec["world"] if backend == "nccl" else None

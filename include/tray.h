@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define TRAY_ABI_VERSION 2 /* 2: tray_render_devices_progress, tray_release_cache */
+#define TRAY_ABI_VERSION 3 /* 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get */
 
 typedef enum tray_status {
     TRAY_OK = 0,
@@ -271,6 +271,28 @@ typedef struct tray_scene_info {
     double bound;         /* M: the BVH needs every ray origin in [-M, M]^3 */
 } tray_scene_info;
 int tray_scene_get_info(tray_scene_t scene, tray_scene_info *out);
+
+/* How a render of `params` (n_passes progressive passes from params->pass) on
+ * `scene` with `camera` would run, without running it. Pixel sums: with
+ * fixed_point_shift k > 0 (rays_per_pixel a multiple of 64 and a colour bound
+ * that allows k >= 44) each pixel's samples are summed exactly as integers of
+ * 2^-k, so the mean is within 2^-(k+1) of the exact mean of the sample colours
+ * whatever order the samples finish in; k = 0: the FP64 sum in sample order of
+ * Go's RenderLines (ray/tracer.go:143). acc_slots > 0: those sums are kept on
+ * chip (per-wave LDS accumulators, one 32-B record per 64 samples in
+ * buffer_bytes); 0: through a 24-B per-sample buffer. Both give the same bits. */
+typedef struct tray_render_plan {
+    int32_t fixed_point_shift; /* k (0: FP64 sum in sample order) */
+    int32_t acc_slots;         /* on-chip accumulators per wave (0: per-sample buffer) */
+    int32_t bvh;               /* 1: the BVH kernel; 0: the reference-order linear scan */
+    int32_t lds_layout;        /* BVH: as tray_scene_info.lds_resident; linear scan: 1 geometry in LDS */
+    int32_t stack_lds;         /* BVH: traversal stack entries per lane kept in LDS */
+    int32_t reserved;          /* 0 */
+    int64_t lds_bytes;         /* dynamic LDS per workgroup */
+    int64_t buffer_bytes;      /* device workspace for the samples or chunk records of one launch band */
+} tray_render_plan;
+int tray_render_plan_get(tray_scene_t scene, const tray_camera *camera, const tray_params *params,
+                         int32_t n_passes, tray_render_plan *out);
 
 /* Asynchronous render into DEVICE memory on `stream` (a hipStream_t, or NULL for
  * the null stream of the scene's device). out_device: compact rows in the

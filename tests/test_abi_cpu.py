@@ -19,7 +19,7 @@ def test_exports_match_header(L):
     lib = L.lib()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.tray_abi_version() == 2  # 2: tray_render_devices_progress, tray_release_cache
+    assert lib.tray_abi_version() == 3  # 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get
 
 
 def _setup(L, arr):
@@ -180,6 +180,7 @@ def test_scene_info_layout(L):
     import ctypes
 
     assert ctypes.sizeof(L.SceneInfo) == 8 * 4 + 8
+    assert ctypes.sizeof(L.RenderPlan) == 6 * 4 + 2 * 8
 
 
 def test_png_sink_round_trip():

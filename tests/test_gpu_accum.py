@@ -122,3 +122,33 @@ def test_passes_and_tiles_with_chunk_partials(L, O):
                         assert np.array_equal(frames[k], one), (band, tiles, k)
     finally:
         dev.release()
+
+
+def test_render_plan(L, O):
+    """tray_render_plan_get reports which accumulation a render runs: the benchmark
+    configs C2-C5 sum on chip, C1 (r = 16) keeps the FP64 sum in sample order."""
+    from bench import CONFIGS
+    from tray_amd import ray
+
+    plans = {}
+    for c in ("c1", "c2", "c5"):
+        _, seed, half, w, h, spp, depth = CONFIGS[c]
+        cam = ray.RichSceneCamera()
+        cam.Initialize(w, h)
+        dev = L.DeviceScene(ray.rich_scene_array(seed, half), ray._background(ray.DefaultBackground()), 0)
+        try:
+            p = L.make_params(w, h, depth, spp, 0.5, seed, output=L.OUT_RGB_F32)
+            plans[c] = dev.plan(cam._state, p, 16).as_dict()
+            with env(TRAY_ACC_SLOTS=0):
+                assert dev.plan(cam._state, p, 16).acc_slots == 0
+            lin = L.make_params(w, h, depth, spp, 0.5, seed, flags=L.FLAG_LINEAR_SCAN)
+            assert dev.plan(cam._state, lin, 1).bvh == 0 and dev.plan(cam._state, lin, 1).acc_slots == 0
+        finally:
+            dev.release()
+    assert plans["c1"]["fixed_point_shift"] == 0 and plans["c1"]["acc_slots"] == 0
+    for c in ("c2", "c5"):
+        assert plans[c]["fixed_point_shift"] == 46 and plans[c]["acc_slots"] >= 8 and plans[c]["bvh"] == 1, plans[c]
+    assert plans["c2"]["lds_layout"] == 1 and plans["c5"]["lds_layout"] == 2
+    # C2, 16 frames: one band, one 32-B record per 64 samples
+    assert plans["c2"]["buffer_bytes"] == 1280 * 720 * 64 * 16 // 64 * 32
+    assert plans["c2"]["lds_bytes"] <= 160 * 1024

@@ -109,6 +109,16 @@ class SceneInfo(ctypes.Structure):
                 ("lds_resident", ctypes.c_int32), ("n_global", ctypes.c_int32), ("bound", ctypes.c_double)]
 
 
+class RenderPlan(ctypes.Structure):
+    """tray_render_plan: how a render would run (pixel sums, kernel, LDS, workspace)."""
+    _fields_ = [("fixed_point_shift", ctypes.c_int32), ("acc_slots", ctypes.c_int32), ("bvh", ctypes.c_int32),
+                ("lds_layout", ctypes.c_int32), ("stack_lds", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("lds_bytes", ctypes.c_int64), ("buffer_bytes", ctypes.c_int64)]
+
+    def as_dict(self) -> dict:
+        return {name: int(getattr(self, name)) for name, _ in self._fields_ if name != "reserved"}
+
+
 class TrayError(RuntimeError):
     def __init__(self, code: int, message: str):
         super().__init__(f"tray error {code}: {message}")
@@ -137,6 +147,7 @@ EXPORTS = (
     "tray_scene_upload",
     "tray_scene_release",
     "tray_scene_get_info",
+    "tray_render_plan_get",
     "tray_render_async",
     "tray_render_passes_async",
     "tray_render_stats_async",
@@ -209,6 +220,9 @@ def lib(path: str | None = None) -> ctypes.CDLL:
     L.tray_scene_release.argtypes = [vp]
     if hasattr(L, "tray_scene_get_info"):  # absent from builds older than this binding (A/B tools)
         L.tray_scene_get_info.argtypes = [vp, ctypes.POINTER(SceneInfo)]
+    if hasattr(L, "tray_render_plan_get"):
+        L.tray_render_plan_get.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), i32,
+                                           ctypes.POINTER(RenderPlan)]
     L.tray_render_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
     L.tray_render_stats_async.argtypes = [vp, ctypes.POINTER(CameraState), ctypes.POINTER(Params), vp, vp, vp]
     if hasattr(L, "tray_render_passes_async"):  # absent from older builds (A/B tools)
@@ -389,6 +403,15 @@ class DeviceScene:
                                             stats_ptr, stream)
         if rc != TRAY_OK:
             raise TrayError(rc, self.L.tray_last_error().decode())
+
+    def plan(self, camera: CameraState, params: Params, n_passes: int = 1) -> RenderPlan:
+        """tray_render_plan_get: how render_async / render_passes_async would run."""
+        out = RenderPlan()
+        rc = self.L.tray_render_plan_get(self.handle, ctypes.byref(camera), ctypes.byref(params), int(n_passes),
+                                         ctypes.byref(out))
+        if rc != TRAY_OK:
+            raise TrayError(rc, self.L.tray_last_error().decode())
+        return out
 
     def info(self) -> SceneInfo:
         out = SceneInfo()

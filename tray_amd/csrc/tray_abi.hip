@@ -485,16 +485,19 @@ static int32_t fixed_point_shift(const tray_scene_s* sc, const tray_params* p) {
     return k >= kAccMinShift ? std::min(k, 600) : 0;
 }
 
-static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
-                             uint32_t* segments_device, unsigned long long* stats_device, void* stream,
-                             int32_t n_passes = 1, unsigned long long* progress_device = nullptr) {
-    if (!sc || !cam || !out_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+// The kernel parameters of a render of `p` on `sc` (everything but the output,
+// instrumentation and workspace pointers) and whether it runs the BVH kernel.
+static int prepare_render(tray_scene_t sc, const tray_camera* cam, const tray_params* p, int32_t n_passes,
+                          KernelParams& k, bool& use_bvh) {
+    if (!sc || !cam) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     int rc = validate_params(p);
     if (rc) return rc;
     if (n_passes < 1) return fail(TRAY_ERR_INVALID_ARGUMENT, "n_passes must be >= 1");
     if (((uint64_t)p->pass + (uint64_t)n_passes) * (uint64_t)p->rays_per_pixel > 0x100000000ull)
         return fail(TRAY_ERR_TOO_LARGE, "(pass + n_passes) x rays_per_pixel exceeds the 32-bit RNG sample word");
-    KernelParams k;
+    const uint64_t spp_launch = (uint64_t)p->rays_per_pixel * (uint64_t)n_passes;
+    if (!band_fits(p->width, spp_launch))
+        return fail(TRAY_ERR_TOO_LARGE, "width x rays_per_pixel x passes too large (8 rows of samples exceed 2^31)");
     memset(&k, 0, sizeof(k));
     k.geo = sc->geo;
     k.mat = sc->mat;
@@ -531,14 +534,10 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
             v->z = std::ldexp(v->z, k.acc_shift);
         }
     }
-    k.out = out_device;
     k.passes = (uint32_t)n_passes;
     k.pass0 = (uint32_t)p->pass;
     k.out_frame_bytes = (size_t)k.rows * (size_t)p->width * bytes_per_pixel(p->output);
-    k.segments = segments_device;
-    k.stats = stats_device;
     k.srgb = sc->srgb;
-    k.progress = progress_device;
     k.nodes = sc->nodes;
     k.bgeo = sc->bgeo;
     k.bidx = sc->bidx;
@@ -557,11 +556,24 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     for (int i = 0; i < 3; ++i) cam_extent = std::max(cam_extent, std::fabs(cam->position[i]));
     cam_extent += std::fabs(cam->defocus_u[0]) + std::fabs(cam->defocus_u[1]) + std::fabs(cam->defocus_u[2]) +
                   std::fabs(cam->defocus_v[0]) + std::fabs(cam->defocus_v[1]) + std::fabs(cam->defocus_v[2]);
-    const bool use_bvh = sc->has_bvh && !(p->flags & TRAY_FLAG_LINEAR_SCAN) && cam_extent <= sc->bvh_bound;
+    use_bvh = sc->has_bvh && !(p->flags & TRAY_FLAG_LINEAR_SCAN) && cam_extent <= sc->bvh_bound;
+    return TRAY_OK;
+}
+
+static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
+                             uint32_t* segments_device, unsigned long long* stats_device, void* stream,
+                             int32_t n_passes = 1, unsigned long long* progress_device = nullptr) {
+    if (!out_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+    KernelParams k;
+    bool use_bvh = false;
+    int rc = prepare_render(sc, cam, p, n_passes, k, use_bvh);
+    if (rc) return rc;
+    k.out = out_device;
+    k.segments = segments_device;
+    k.stats = stats_device;
+    k.progress = progress_device;
     TRAY_HIP(hipSetDevice(sc->device));
     const uint64_t spp_launch = (uint64_t)p->rays_per_pixel * (uint64_t)n_passes;
-    if (!band_fits(p->width, spp_launch))
-        return fail(TRAY_ERR_TOO_LARGE, "width x rays_per_pixel x passes too large (8 rows of samples exceed 2^31)");
     const size_t need = accum_buffer_bytes(p->width, k.rows, spp_launch, launch_layout(k, use_bvh).acc_slots > 0);
     if (need > sc->samples_bytes) {
         if (sc->samples) {
@@ -603,6 +615,26 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         k.cand = sc->cand;
     }
     TRAY_HIP(launch_render(k, use_bvh, static_cast<hipStream_t>(stream)));
+    return TRAY_OK;
+}
+
+int tray_render_plan_get(tray_scene_t sc, const tray_camera* cam, const tray_params* p, int32_t n_passes,
+                         tray_render_plan* out) {
+    if (!out) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
+    memset(out, 0, sizeof(*out));
+    KernelParams k;
+    bool use_bvh = false;
+    int rc = prepare_render(sc, cam, p, n_passes, k, use_bvh);
+    if (rc) return rc;
+    const LaunchLayout L = launch_layout(k, use_bvh);
+    out->fixed_point_shift = k.acc_shift;
+    out->acc_slots = L.acc_slots;
+    out->bvh = use_bvh ? 1 : 0;
+    out->lds_layout = L.lds_mode;
+    out->stack_lds = use_bvh ? L.stack_lds : 0;
+    out->lds_bytes = (int64_t)L.lds;
+    out->buffer_bytes = (int64_t)accum_buffer_bytes(p->width, k.rows, (uint64_t)p->rays_per_pixel * (uint64_t)n_passes,
+                                                    L.acc_slots > 0);
     return TRAY_OK;
 }
 
