@@ -427,6 +427,13 @@ def main() -> int:
                                   "note": "NOT a roofline fraction: the reference's work (every sphere tested per "
                                           "segment) over the measured time; the BVH skips ~99.7 % of it exactly"},
         }
+        # BASELINE.md's secondary metrics, over the same timed launch
+        sec = kernel_ms * 1e-3
+        rec["secondary"] = {"segments_per_s": round(segments_local / sec, 1),
+                            "sphere_tests_per_s": round(sphere_tests / sec, 1),
+                            "box_tests_per_s": round(box_tests / sec, 1),
+                            "segments_per_sample": round(segments_local / local_samples, 4),
+                            "scope": "rank 0's rows, one launch of F frames (kernel_ms)"}
         if util:
             roof["valu_issue_util"] = util.get("valu_issue_utilisation")
             roof["lane_util"] = util.get("valu_lane_utilisation")
