@@ -75,3 +75,77 @@ def test_random_scene_vs_oracle(L, O, k):
     assert np.array_equal(np.isfinite(rgb), finite), k
     err = float(np.max(np.abs(rgb[finite] - ref[finite]))) if finite.any() else 0.0
     assert err <= TIGHT, (k, err)
+
+
+# Fixed-point pixel sums (64 | r; DESIGN.md §5 "Accumulation") on random scenes:
+# backgrounds up to 12 and albedos up to 1.1 move the colour bound, so the scale
+# 2^k ranges over its limits and some cases fall back to the FP64 sum in sample
+# order (tray_render_plan_get says which). Same bar; the fixed-point frames are
+# also compared with the device's own FP64-order frames (TRAY_FIXED_POINT=0).
+N_FIXED = 16
+
+
+@pytest.mark.parametrize("k", range(N_FIXED))
+def test_random_scene_fixed_point_vs_oracle(L, O, k):
+    import os
+
+    rng = np.random.default_rng(5000 + k)
+    n = [3, 24, 160, 600][k % 4]
+    spheres = random_scene(O, rng, n, ground=k % 3 != 2)
+    if k % 4 == 1:  # albedo above 1: the bound grows with the depth
+        spheres["albedo"] *= rng.uniform(1.0, 1.1)
+    setup = random_setup(rng, spheres, inside=k % 5 == 4)
+    w, h = int(rng.integers(9, 25)), int(rng.integers(5, 17))
+    spp, depth = int(rng.choice([64, 128])), int(rng.choice([3, 10, 50]))
+    radius = float(rng.choice([0.0, 0.5, 1.7]))
+    seed = int(rng.integers(0, 2**63))
+    bg = np.r_[rng.uniform(0, 1, 3), rng.uniform(0, 1, 3)] * float(rng.choice([0.3, 1.0, 4.0, 12.0]))
+    st = camera(L, setup, w, h)
+    p = L.make_params(w, h, depth, spp, radius, seed)
+    dev = L.DeviceScene(spheres, bg_struct(L, bg), 0)
+    try:
+        shift = dev.plan(st, p).fixed_point_shift
+    finally:
+        dev.release()
+    att = max(1.0, float(np.abs(spheres["albedo"][spheres["material"] != 3]).max(initial=0.0)))
+    bound = float(np.abs(bg).max()) * att ** depth * 1.001
+    assert (shift > 0) == (bound < 2.0 ** (47 - 44)), (k, shift, bound)
+    rgb, seg = L.render(spheres, bg_struct(L, bg), st, p, 0, segments=True)
+    os.environ["TRAY_FIXED_POINT"] = "0"
+    try:
+        f64, seg2 = L.render(spheres, bg_struct(L, bg), st, p, 0, segments=True)
+    finally:
+        del os.environ["TRAY_FIXED_POINT"]
+    ref, rseg = O.render(spheres, bg, st.as_array(), w, h, spp, depth, radius, seed, workers=WORKERS)
+    assert np.array_equal(seg, rseg) and np.array_equal(seg2, rseg), k
+    finite = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(rgb), finite) and np.array_equal(np.isfinite(f64), finite), k
+    scale = max(1.0, float(np.abs(ref[finite]).max())) if finite.any() else 1.0
+    err = float(np.max(np.abs(rgb[finite] - ref[finite]))) if finite.any() else 0.0
+    assert err <= TIGHT * scale, (k, shift, err)
+    if shift > 0:
+        assert float(np.max(np.abs(rgb[finite] - f64[finite]), initial=0.0)) <= 2.0 ** (-shift + 1), k
+    else:
+        assert np.array_equal(rgb, f64, equal_nan=True), k
+
+
+def test_degenerate_camera_nan_in_both_sums(L, O):
+    """Up parallel to the view direction: Go's camera basis u = Unit(Cross(Up, w))
+    is NaN (ray/camera.go:80), so every colour is NaN; the fixed-point sums
+    (r = 64) give NaN in the same channels as the FP64 sum and the oracle."""
+    import os
+
+    sc = O.rich_scene(2)
+    setup = np.array([0.0, 5, 0, 0, 0, 0, 0, 1, 0, 20.0, 10.0, 10.0, 0.1])
+    w, h = 12, 8
+    st = camera(L, setup, w, h)
+    p = L.make_params(w, h, 10, 64, 0.5, 3)
+    bg = np.array([1.0, 1.0, 1.0, 0.4, 0.65, 1.0])
+    rgb, _ = L.render(sc, bg_struct(L, bg), st, p, 0, segments=True)
+    os.environ["TRAY_FIXED_POINT"] = "0"
+    try:
+        f64, _ = L.render(sc, bg_struct(L, bg), st, p, 0, segments=True)
+    finally:
+        del os.environ["TRAY_FIXED_POINT"]
+    ref, _ = O.render(sc, bg, st.as_array(), w, h, 64, 10, 0.5, 3, workers=WORKERS)
+    assert np.array_equal(np.isfinite(rgb), np.isfinite(ref)) and np.array_equal(np.isfinite(f64), np.isfinite(ref))
