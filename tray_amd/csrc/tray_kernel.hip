@@ -1383,7 +1383,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             {
                 PROF_T0();
                 TRAY_MARK("node_ctl")
-#pragma unroll 1
+                // Unrolled: the steps are straight-line code (no loop counter, and the
+                // compiler schedules across them; C2 -0.9 %, C5 -0.8 % against a rolled loop).
+#pragma unroll
                 for (int s = 0; s < TRAY_NODE_STEPS_MAX; ++s) {
                     const uint64_t m = __ballot(is_trav(T.cur));
                     if (m == 0ull) break;
