@@ -876,6 +876,9 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
 #ifndef TRAY_EARLY_MAT
 #define TRAY_EARLY_MAT 1
 #endif
+#ifndef TRAY_LAZY_UD
+#define TRAY_LAZY_UD 1
+#endif
 template <bool kStats, bool kAcc, typename GeoAt, typename MatAt>
 __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
                                            double dir_lsq, GeoAt geo_at, MatAt mat_at, Stats& st, const AccCtx& acc) {
@@ -893,7 +896,15 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #endif
     const Block w = philox4x32_10(uni_seed(uni), L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
     const double u0 = uniform(w.x0);
+#if TRAY_LAZY_UD
+    // Unit(r.Direction) is read by the sky, Metal and Dielectric, not by Lambertian
+    // (nor a last-level hit): a wave whose shading lanes are all Lambertian hits
+    // (a camera-ray pass of a diffuse pixel) skips the sqrt and three quotients.
+    D3 ud = d3(0, 0, 0);
+    if (!hit || (!last && m.type != kLambertian)) ud = unit_lsq(L.dir, dir_lsq);
+#else
     const D3 ud = unit_lsq(L.dir, dir_lsq);  // dir_lsq = length_sq(L.dir), the segment's `a`
+#endif
     D3 color = d3(0, 0, 0);
     if (!hit) {  // AmbientLight.Hit (ray/objects.go:68-73)
         const double t = 0.5 * (ud.y + 1.0);
@@ -966,12 +977,13 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #ifndef TRAY_NODE_STEPS
 #define TRAY_NODE_STEPS 3
 #endif
-// Up to TRAY_NODE_STEPS_MAX node steps while at least TRAY_NODE_MORE_LANES lanes still traverse.
+// Up to TRAY_NODE_STEPS_MAX node steps while at least TRAY_NODE_MORE_LANES lanes still traverse
+// (the steps unrolled; against a fixed 3: C2 -2.8 %, C5 -0.8 %, DESIGN.md §5 log).
 #ifndef TRAY_NODE_STEPS_MAX
-#define TRAY_NODE_STEPS_MAX TRAY_NODE_STEPS
+#define TRAY_NODE_STEPS_MAX 5
 #endif
 #ifndef TRAY_NODE_MORE_LANES
-#define TRAY_NODE_MORE_LANES 64
+#define TRAY_NODE_MORE_LANES 8
 #endif
 #ifndef TRAY_LEAF_BATCH
 #define TRAY_LEAF_BATCH 20
