@@ -982,6 +982,11 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
 #ifndef TRAY_NODE_STEPS_MAX
 #define TRAY_NODE_STEPS_MAX 5
 #endif
+// Trees of more than kDeepNodes nodes (more node visits per segment: C5's 514-node tree against the
+// book cover's 260) run a kernel instance with one more node step (C5 -1.6 %; the same step on the
+// book cover costs +0.3 %, and a runtime cap in one instance cost the book cover 0.8 %).
+constexpr int kDeepSteps = TRAY_NODE_STEPS_MAX + 1;
+constexpr int32_t kDeepNodes = 384;
 #ifndef TRAY_NODE_MORE_LANES
 #define TRAY_NODE_MORE_LANES 8
 #endif
@@ -1079,7 +1084,8 @@ __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (si
 // kProg: the live-progress instance (tray_render_progress only), so the other
 // instances carry no progress code or registers.
 // kAcc: on-chip fixed-point accumulation of each 64-sample chunk (end_path).
-template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg, bool kAcc>
+// kSteps: node steps per loop iteration at most (kDeepSteps for deep trees, launch_render).
+template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg, bool kAcc, int kSteps = TRAY_NODE_STEPS_MAX>
 __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
     extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
     __attribute__((address_space(3))) Uniforms* uni_lds =
@@ -1402,7 +1408,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 // Unrolled: the steps are straight-line code (no loop counter, and the
                 // compiler schedules across them; C2 -0.9 %, C5 -0.8 % against a rolled loop).
 #pragma unroll
-                for (int s = 0; s < TRAY_NODE_STEPS_MAX; ++s) {
+                for (int s = 0; s < kSteps; ++s) {
                     const uint64_t m = __ballot(is_trav(T.cur));
                     if (m == 0ull) break;
                     if (s >= TRAY_NODE_STEPS && __popcll(m) < TRAY_NODE_MORE_LANES) break;
@@ -1863,31 +1869,37 @@ hipError_t launch_to_srgba(const double* rgb, size_t n_pixels, uint32_t* rgba, c
 
 using KernelFn = void (*)(KernelParams);
 
-template <bool kBVH, bool kSpill, bool kStats, bool kProg, bool kAcc>
-static KernelFn pick_kernel3(int lds_mode) {
-    if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill, kProg, kAcc>;
+template <bool kBVH, bool kSpill, bool kStats, bool kProg, bool kAcc, int kSteps>
+static KernelFn pick_kernel4(int lds_mode) {
+    if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
     if constexpr (kBVH)
-        if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill, kProg, kAcc>;
-    return render_kernel<0, kBVH, kStats, kSpill, kProg, kAcc>;
+        if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
+    return render_kernel<0, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
+}
+template <bool kBVH, bool kSpill, bool kStats, bool kProg, bool kAcc>
+static KernelFn pick_kernel3(int lds_mode, bool deep) {
+    if constexpr (kBVH && !kSpill)
+        if (deep) return pick_kernel4<kBVH, kSpill, kStats, kProg, kAcc, kDeepSteps>(lds_mode);
+    return pick_kernel4<kBVH, kSpill, kStats, kProg, kAcc, TRAY_NODE_STEPS_MAX>(lds_mode);
 }
 
 // Instrumentation: the stats instance counts segments and tests; the progress
 // instance feeds tray_render_progress; neither is ever timed by the bench.
 template <bool kBVH, bool kSpill, bool kAcc>
-static KernelFn pick_kernel2(int lds_mode, bool stats, bool progress) {
-    if (stats) return pick_kernel3<kBVH, kSpill, true, false, kAcc>(lds_mode);
-    if (progress) return pick_kernel3<kBVH, kSpill, false, true, kAcc>(lds_mode);
-    return pick_kernel3<kBVH, kSpill, false, false, kAcc>(lds_mode);
+static KernelFn pick_kernel2(int lds_mode, bool stats, bool progress, bool deep) {
+    if (stats) return pick_kernel3<kBVH, kSpill, true, false, kAcc>(lds_mode, deep);
+    if (progress) return pick_kernel3<kBVH, kSpill, false, true, kAcc>(lds_mode, deep);
+    return pick_kernel3<kBVH, kSpill, false, false, kAcc>(lds_mode, deep);
 }
 
 // On-chip accumulation is built for the BVH kernel with the whole stack on
 // chip (launch_layout grants accumulators only then); every other launch sums
 // through the per-sample buffer.
-static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, bool spill, bool acc) {
-    if (!bvh) return pick_kernel2<false, false, false>(lds_mode, stats, progress);
-    if (spill) return pick_kernel2<true, true, false>(lds_mode, stats, progress);
-    return acc ? pick_kernel2<true, false, true>(lds_mode, stats, progress)
-               : pick_kernel2<true, false, false>(lds_mode, stats, progress);
+static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, bool spill, bool acc, bool deep) {
+    if (!bvh) return pick_kernel2<false, false, false>(lds_mode, stats, progress, false);
+    if (spill) return pick_kernel2<true, true, false>(lds_mode, stats, progress, false);
+    return acc ? pick_kernel2<true, false, true>(lds_mode, stats, progress, deep)
+               : pick_kernel2<true, false, false>(lds_mode, stats, progress, deep);
 }
 
 template <int kMode>
@@ -2061,8 +2073,11 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (use_bvh && p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
+    bool deep = use_bvh && p.n_nodes > kDeepNodes;
+    if (const char* e = getenv("TRAY_NODE_DEEP"))  // A/B: force the instance
+        deep = use_bvh && atoi(e) != 0;
     const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr,
-                                    use_bvh && p.stack_cap > p.stack_lds, p.acc_slots > 0);
+                                    use_bvh && p.stack_cap > p.stack_lds, p.acc_slots > 0, deep);
     const KernelFn resolve = pick_resolve(p);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {
