@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-phase ISA census of the BVH megakernel (render_kernel<1,true,false,false,false,true>).
+"""Per-phase ISA census of the BVH megakernel (render_kernel<1,true,false,false,false,true,5>).
 
 Builds tray_kernel.hip for gfx950 with the product flags plus -g (debug line
 tables do not change the generated code: the census checks the instruction
@@ -38,7 +38,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tray_amd", "csrc", "tray_kernel.hip")
-KERNEL = "_ZN4tray13render_kernelILi1ELb1ELb0ELb0ELb0ELb1EEEvNS_12KernelParamsE"  # --layout 2: ...ILi2E...
+KERNEL = "_ZN4tray13render_kernelILi1ELb1ELb0ELb0ELb0ELb1ELi5EEEvNS_12KernelParamsE"  # --layout 2: ...ILi2E...
 LLVM = "/opt/rocm/lib/llvm/bin"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", "-mllvm",
          "-amdgpu-atomic-optimizer-strategy=None"]

@@ -24,9 +24,9 @@ def main():
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"]
             # the timed kernel: render_kernel<mode, true, false (no stats), spill>
-            # the timed BVH kernel: render_kernel<layout, true, false (no stats), false (no spill), false, true (on-chip sums)>
+            # the timed BVH kernel: render_kernel<layout, true, false (no stats), false (no spill), false, true (on-chip sums), S (node steps)>
             # (layout 1 for the book cover, 2 for the dense C5 scene)
-            if "render_kernel<" not in name or ", true, false, false, false, true>" not in name:
+            if "render_kernel<" not in name or ", true, false, false, false, true, " not in name:
                 continue
             kernel = name
             key = (row["Counter_Name"], row["Dispatch_Id"])

@@ -18,7 +18,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = ", true, false, false, false, true>"  # the timed BVH kernel (on-chip accumulation), any LDS layout (1: book cover, 2: dense C5)
+KERNEL = ", true, false, false, false, true, "  # the timed BVH kernel (on-chip accumulation), any LDS layout (1: book cover, 2: dense C5) and step count
 
 
 def values(path):
@@ -61,7 +61,7 @@ def main():
     rec = {
         "config": args.config,
         "frames_per_launch": args.frames,
-        "kernel": "tray::render_kernel<L, true, false, false, false, true> (BVH, LDS layout L, no stack spill, on-chip accumulation)",
+        "kernel": "tray::render_kernel<L, true, false, false, false, true, S> (BVH, LDS layout L, no stack spill, on-chip accumulation, S node steps)",
         "bands_per_launch": bands,
         "FETCH_SIZE_KB_raw_per_dispatch": fetch_kb,
         "WRITE_SIZE_KB_per_dispatch": write_kb,
