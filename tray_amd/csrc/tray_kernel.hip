@@ -1001,7 +1001,8 @@ constexpr int32_t kDeepNodes = 384;
 #define TRAY_REFILL_BATCH 24
 #endif
 // Below TRAY_TRAV_SPARSE traversing lanes (node steps mostly empty) the leaf and shade phases
-// already run from TRAY_LEAF_LOW / TRAY_SHADE_LOW waiting lanes (TRAY_SHADE_LOW 64: shade batches unchanged).
+// already run from TRAY_LEAF_LOW / TRAY_SHADE_LOW waiting lanes (with the adaptive node steps the
+// loop leaves its steps exactly then; shading from 32: C2 -0.4 %, C5 -0.65 %).
 #ifndef TRAY_TRAV_SPARSE
 #define TRAY_TRAV_SPARSE 8
 #endif
@@ -1009,7 +1010,7 @@ constexpr int32_t kDeepNodes = 384;
 #define TRAY_LEAF_LOW 8
 #endif
 #ifndef TRAY_SHADE_LOW
-#define TRAY_SHADE_LOW 64
+#define TRAY_SHADE_LOW 32
 #endif
 // Camera rays answered by their candidate list are shaded inside the refill phase (1) or wait for
 // the shade phase (0).
