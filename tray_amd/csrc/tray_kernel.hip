@@ -344,7 +344,7 @@ struct SceneView {
     const double4* geo;     // linear scan: list order, NaN-padded
     const Bvh4Node* nodes;  // BVH: 4-wide nodes, root first
     const int32_t* leaves;  // BVH: per leaf (first slot << 3) | count
-    bool single;            // BVH: one sphere per leaf, leaf index == slot
+    int32_t leaf_mode;      // BVH: KernelParams::leaf_single (1: one sphere per leaf, leaf index == slot)
     const double4* bgeo;    // BVH: spheres in leaf-slot order
     const int32_t* bidx;    // BVH: original list index of each slot
     const MatRec* bmat;     // BVH: shading record of each slot
@@ -660,12 +660,20 @@ template <class Stk>
 __device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const Stk& S, const D3& org,
                                               const D3& dir, uint32_t& tested) {
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for the pop
-    if (sv.single) {  // one sphere per leaf: the leaf index is its slot (no leaf table, no loop)
+    if (sv.leaf_mode == 1) {  // one sphere per leaf: the leaf index is its slot (no leaf table, no loop)
         test_slot(T, sv, (int32_t)(T.cur & (kBvhLeafBit - 1u)), org, dir);
         tested = 1;
     } else {
-        const int32_t info = sv.leaves[T.cur & (kBvhLeafBit - 1u)];
-        const int32_t first = info >> 3, cnt = info & 7;
+        const uint32_t ref = T.cur & (kBvhLeafBit - 1u);
+        int32_t first, cnt;
+        if (sv.leaf_mode == 2) {  // the reference is the leaf (bvh_leaf_direct)
+            first = (int32_t)(ref >> 2);
+            cnt = (int32_t)(ref & 3u) + 1;
+        } else {
+            const int32_t info = sv.leaves[ref];
+            first = info >> 3;
+            cnt = info & 7;
+        }
         tested = 0;
         // Two spheres per step, both loads issued before either test: with the
         // geometry in global memory (dense scenes) a leaf's spheres are then one
@@ -1120,7 +1128,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         u->pool_chunks = p.pool_chunks;
     }
     const UniPtr uni = uni_lds;
-    SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single != 0,       p.bgeo, p.bidx,
+    SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single,            p.bgeo, p.bidx,
                  p.bmat, p.n,     p.n_nodes,   p.n_global, p.n_slots - p.n_global};
     Stack<kSpill> S{nullptr, nullptr, 0, 0};
     if constexpr (kBVH) {
