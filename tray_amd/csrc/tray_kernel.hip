@@ -1027,6 +1027,9 @@ constexpr int32_t kDeepNodes = 384;
 #ifndef TRAY_PRIO_LEAF
 #define TRAY_PRIO_LEAF 1
 #endif
+#ifndef TRAY_SKIP_PADDING
+#define TRAY_SKIP_PADDING 1
+#endif
 // Camera rays answered by their candidate list are shaded inside the refill phase (1) or wait for
 // the shade phase (0).
 #ifndef TRAY_REFILL_SHADE
@@ -1263,6 +1266,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         acc_free &= ~(1ull << pool_slot);
                         acc_chunk = lane == pool_slot ? c : acc_chunk;
                     }
+#if TRAY_SKIP_PADDING
+                    else {
+                        // A padding chunk (the last tile row of a band whose rows are not a
+                        // multiple of 8, e.g. a 90-row shard): skip it instead of handing its
+                        // items to lanes that would idle through an iteration.
+                        pool_next = pool_end;
+                        continue;
+                    }
+#endif
                 }
             }
             const uint32_t n_idle = (uint32_t)__popcll(idle);
