@@ -22,23 +22,11 @@ constexpr int kBvhLeafMax = 4;
 // Below this many spheres the linear scan is used (no BVH is built).
 constexpr int kBvhMinSpheres = 16;
 // Child references are 16 bits: an inner node index (< 0x8000), 0x8000 | leaf
-// index (or the leaf itself, bvh_leaf_direct), or kBvhNone for an unused child
-// slot (whose box is empty).
+// index, or kBvhNone for an unused child slot (whose box is empty).
 constexpr uint32_t kBvhLeafBit = 0x8000u;
 constexpr uint32_t kBvhNone = 0xFFFFu;
 constexpr int32_t kBvhMaxNodes = 0x8000;
 constexpr int32_t kBvhMaxLeaves = 0x7FFF;
-// Multi-sphere leaves of a scene with fewer than 2^13 slots are referenced
-// directly, 0x8000 | first slot << 2 | (count - 1), so a leaf visit reads no
-// leaf table before its geometry (one dependent LDS round trip fewer).
-#ifndef TRAY_LEAF_DIRECT
-#define TRAY_LEAF_DIRECT 1
-#endif
-constexpr int32_t kBvhDirectSlots = 0x1FFF;
-static_assert(kBvhLeafMax <= 4, "direct leaf references hold count - 1 in 2 bits");
-inline bool bvh_leaf_direct(int leaf_max, int32_t n_slots) {
-    return TRAY_LEAF_DIRECT && leaf_max > 1 && n_slots <= kBvhDirectSlots;
-}
 // A sphere whose box dwarfs the rest of the scene (a ground sphere) is not put
 // in the tree: every traversal tests it first (nearly every ray would visit
 // it anyway), which also seeds the culling distance. At most kBvhGlobals, each

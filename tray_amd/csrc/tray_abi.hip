@@ -547,7 +547,7 @@ static int prepare_render(tray_scene_t sc, const tray_camera* cam, const tray_pa
     k.n_leaves = sc->n_leaves;
     k.n_global = sc->n_global;
     k.leaves = sc->leaves;
-    k.leaf_single = sc->leaf_max == 1 ? 1 : bvh_leaf_direct(sc->leaf_max, sc->n_slots) ? 2 : 0;
+    k.leaf_single = sc->leaf_max == 1 ? 1 : 0;
     k.stack_ovf = sc->stack_ovf;
     k.stack_cap = sc->stack_cap;
     // The BVH's conservative FP32 box test assumes every ray origin lies within

@@ -80,7 +80,6 @@ struct Builder {
     std::vector<int32_t> idx;
     double pad = 0;
     int leaf_max = 1;
-    bool direct = false;  // leaf references hold the leaf (bvh_leaf_direct)
     int32_t stack_max = 0;
 
     static float down(double v) {
@@ -245,8 +244,7 @@ struct Builder {
                     geo.push_back(make_double4(sp.center[0], sp.center[1], sp.center[2], sp.radius * sp.radius));
                     idx.push_back(prims[i].index);
                 }
-                nodes[me].ref[k] = direct ? kBvhLeafBit | ((uint32_t)slot << 2) | (uint32_t)(c.count - 1)
-                                          : kBvhLeafBit | (uint32_t)leaves.size();
+                nodes[me].ref[k] = kBvhLeafBit | (uint32_t)leaves.size();
                 leaves.push_back((slot << 3) | c.count);
             } else {
                 const int sub = collapse(ch[k], here, s);
@@ -286,7 +284,6 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     m = std::max(m, 1.0);
     B.pad = 4e-6 * m;
     B.leaf_max = std::min(std::max(leaf_max, 1), kBvhLeafMax);
-    B.direct = bvh_leaf_direct(B.leaf_max, n);  // slots: the n spheres
     std::vector<Prim> globals;
     while ((int)globals.size() < kBvhGlobals && (int)B.prims.size() > B.leaf_max + 1) {
         size_t big = 0;

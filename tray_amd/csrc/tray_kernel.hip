@@ -344,7 +344,7 @@ struct SceneView {
     const double4* geo;     // linear scan: list order, NaN-padded
     const Bvh4Node* nodes;  // BVH: 4-wide nodes, root first
     const int32_t* leaves;  // BVH: per leaf (first slot << 3) | count
-    int32_t leaf_mode;      // BVH: KernelParams::leaf_single (1: one sphere per leaf, leaf index == slot)
+    bool single;            // BVH: one sphere per leaf, leaf index == slot
     const double4* bgeo;    // BVH: spheres in leaf-slot order
     const int32_t* bidx;    // BVH: original list index of each slot
     const MatRec* bmat;     // BVH: shading record of each slot
@@ -660,20 +660,12 @@ template <class Stk>
 __device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const Stk& S, const D3& org,
                                               const D3& dir, uint32_t& tested) {
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for the pop
-    if (sv.leaf_mode == 1) {  // one sphere per leaf: the leaf index is its slot (no leaf table, no loop)
+    if (sv.single) {  // one sphere per leaf: the leaf index is its slot (no leaf table, no loop)
         test_slot(T, sv, (int32_t)(T.cur & (kBvhLeafBit - 1u)), org, dir);
         tested = 1;
     } else {
-        const uint32_t ref = T.cur & (kBvhLeafBit - 1u);
-        int32_t first, cnt;
-        if (sv.leaf_mode == 2) {  // the reference is the leaf (bvh_leaf_direct)
-            first = (int32_t)(ref >> 2);
-            cnt = (int32_t)(ref & 3u) + 1;
-        } else {
-            const int32_t info = sv.leaves[ref];
-            first = info >> 3;
-            cnt = info & 7;
-        }
+        const int32_t info = sv.leaves[T.cur & (kBvhLeafBit - 1u)];
+        const int32_t first = info >> 3, cnt = info & 7;
         tested = 0;
         // Two spheres per step, both loads issued before either test: with the
         // geometry in global memory (dense scenes) a leaf's spheres are then one
@@ -1027,9 +1019,6 @@ constexpr int32_t kDeepNodes = 384;
 #ifndef TRAY_PRIO_LEAF
 #define TRAY_PRIO_LEAF 1
 #endif
-#ifndef TRAY_SKIP_PADDING
-#define TRAY_SKIP_PADDING 1
-#endif
 // Camera rays answered by their candidate list are shaded inside the refill phase (1) or wait for
 // the shade phase (0).
 #ifndef TRAY_REFILL_SHADE
@@ -1131,7 +1120,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         u->pool_chunks = p.pool_chunks;
     }
     const UniPtr uni = uni_lds;
-    SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single,            p.bgeo, p.bidx,
+    SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single != 0,       p.bgeo, p.bidx,
                  p.bmat, p.n,     p.n_nodes,   p.n_global, p.n_slots - p.n_global};
     Stack<kSpill> S{nullptr, nullptr, 0, 0};
     if constexpr (kBVH) {
@@ -1266,15 +1255,6 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         acc_free &= ~(1ull << pool_slot);
                         acc_chunk = lane == pool_slot ? c : acc_chunk;
                     }
-#if TRAY_SKIP_PADDING
-                    else {
-                        // A padding chunk (the last tile row of a band whose rows are not a
-                        // multiple of 8, e.g. a 90-row shard): skip it instead of handing its
-                        // items to lanes that would idle through an iteration.
-                        pool_next = pool_end;
-                        continue;
-                    }
-#endif
                 }
             }
             const uint32_t n_idle = (uint32_t)__popcll(idle);

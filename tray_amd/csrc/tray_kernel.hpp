@@ -107,8 +107,7 @@ struct KernelParams {
     uint32_t acc_off;    // byte offset of the accumulator region in the kernel's dynamic LDS
     const Bvh4Node* nodes;  // exact-culling 4-wide BVH (tray_bvh.cpp), root first
     const int32_t* leaves;  // per leaf: (first slot << 3) | count
-    int32_t leaf_single;    // 1: every leaf holds one sphere and its index is its slot; 2: leaf references
-                            // hold (first slot << 2) | (count - 1) (bvh_leaf_direct); 0: the leaf table
+    int32_t leaf_single;    // 1: every leaf holds one sphere and its index is its slot
     const double4* bgeo;    // spheres in leaf-slot order
     const int32_t* bidx;    // original index per slot
     const MatRec* bmat;     // shading record per slot
