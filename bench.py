@@ -100,16 +100,22 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def _profile_json(name, config, frames):
-    """profiles/<name>_<config>.json when it was measured on this launch shape (N = 1, F frames/launch)."""
-    path = os.path.join(ROOT, "profiles", f"{name}_{config}.json")
+def _profile_json(name, config, frames, code_hash, profiles_dir=None):
+    """profiles/<name>_<config>.json when it was measured on this launch shape (N = 1,
+    F frames/launch) AND on the device code the process loaded (the record's
+    code_object_sha256 equals the library's; tools/pmc_summary.py, pmc_mix.py).
+    Returns (record or None, source path or None, reason when None)."""
+    path = os.path.join(profiles_dir or os.path.join(ROOT, "profiles"), f"{name}_{config}.json")
     try:
         rec = json.load(open(path))
     except (OSError, ValueError):
-        return None, None
+        return None, None, f"no {os.path.basename(path)}"
     if rec.get("frames_per_launch", 1) != frames:
-        return None, None
-    return rec, os.path.relpath(path, ROOT)
+        return None, None, f"{os.path.basename(path)} was measured at {rec.get('frames_per_launch', 1)} frames per launch"
+    if not code_hash or rec.get("code_object_sha256") != code_hash:
+        return None, None, (f"{os.path.basename(path)} was measured on device code "
+                            f"{str(rec.get('code_object_sha256'))[:12]}, the loaded library is {str(code_hash)[:12]}")
+    return rec, os.path.relpath(path, ROOT), None
 
 
 def free_port() -> int:
@@ -387,10 +393,14 @@ def main() -> int:
         achieved = ops / (kernel_ms * 1e-3) / 1e12
         alg_bytes = rows * W * 12 * F  # the float3 frames the launch writes
         traffic = util = pmc_src = mix_src = None
+        code_hash = _lib.code_object_sha256(_lib.LIB_PATH)
+        why_null = {}
         if world == 1:
-            pmc, pmc_src = _profile_json("pmc", args.config, F)
+            pmc, pmc_src, why_null["traffic"] = _profile_json("pmc", args.config, F, code_hash)
             traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-            util, mix_src = _profile_json("pmc_mix", args.config, F)
+            util, mix_src, why_null["util"] = _profile_json("pmc_mix", args.config, F, code_hash)
+        else:
+            why_null = {"traffic": "counters are profiled at N = 1", "util": "counters are profiled at N = 1"}
         roof = {
             "bound": "valu",
             "achieved": round(achieved, 3),
@@ -398,6 +408,11 @@ def main() -> int:
             "unit": "TFLOP/s",
             "frac": round(achieved / FP64_PEAK_OPS, 4),
             "traffic": traffic,
+            # achieved HBM bandwidth of the megakernel launch against the 8 TB/s roof (PMC bytes / launch time)
+            "hbm_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic else None,
+            "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if traffic else None,
+            "hbm_peak_gbs": HBM_PEAK_GBS,
+            "code_object_sha256": code_hash,
             "kernel_ms": round(kernel_ms, 4),
             "frames_per_launch": F,
             "peak_measured": FP64_PEAK_MEASURED,
@@ -438,8 +453,13 @@ def main() -> int:
             roof["valu_issue_util"] = util.get("valu_issue_utilisation")
             roof["lane_util"] = util.get("valu_lane_utilisation")
             roof["util_source"] = mix_src
+        else:
+            roof["valu_issue_util"] = roof["lane_util"] = None
+            roof["util_null_reason"] = why_null.get("util")
         if traffic:
             roof["traffic_source"] = pmc_src
+        else:
+            roof["traffic_null_reason"] = why_null.get("traffic")
         rec["roofline"] = roof
         if world == 1 and not args.no_e2e:
             rec["e2e"] = e2e_timings(_lib, spheres, bg, cam, W, H, depth, spp, seed)

@@ -59,7 +59,8 @@
 extern "C" {
 #endif
 
-#define TRAY_ABI_VERSION 3 /* 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get */
+#define TRAY_ABI_VERSION 4 /* 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get;
+                              4: TRAY_FLAG_ORDERED_SUM (the library no longer reads the process environment) */
 
 typedef enum tray_status {
     TRAY_OK = 0,
@@ -156,6 +157,19 @@ typedef struct tray_params {
  * ray/objects.go:37-46) instead of the exact-culling BVH. Both give identical
  * results; the flag exists for verification and A/B timing. */
 #define TRAY_FLAG_LINEAR_SCAN 1
+
+/* Pixel sums. DEFAULT (flag clear): when rays_per_pixel is a multiple of 64 and
+ * the scene's colour bound allows it, each pixel's samples are summed exactly
+ * as fixed-point integers of 2^-k (k >= 44), so the mean is within 2^-(k+1) of
+ * the exact mean of the sample colours and does not depend on the order in
+ * which samples finish (tray_render_plan_get reports k; C2: k = 46, L-inf
+ * 6.7e-15 against the sequential FP64 sum). With TRAY_FLAG_ORDERED_SUM the
+ * samples are added in sample order in FP64, exactly as Go's RenderLines
+ * accumulates colorSum (ray/tracer.go:143), at the cost of a 24-B per-sample
+ * device buffer. Renders whose r is not a multiple of 64 always use the
+ * ordered sum. Both are far inside the 1e-4 parity gate; the flag selects the
+ * bits. */
+#define TRAY_FLAG_ORDERED_SUM 2
 
 typedef struct tray_scene_s *tray_scene_t;
 

@@ -1,0 +1,44 @@
+/*
+ * tray_debug.h — test and A/B hooks of libtray_amd.so. NOT part of the stable
+ * C-ABI in tray.h: names and meanings may change with any build, and a
+ * production caller (e.g. the cgo shim of INTEGRATION.md) never calls them.
+ *
+ * The library never reads the process environment: a stray TRAY_* variable in a
+ * host process cannot change what it renders. The knobs below are process-wide
+ * and apply to renders started after the call; unset knobs keep the product
+ * behaviour. Each knob overrides one decision the library otherwise makes
+ * itself; the frames they produce stay bit-identical to the defaults unless
+ * noted (tests/test_gpu_*.py check exactly that).
+ *
+ *   "acc_slots"           on-chip chunk accumulators per wave (0 = off: chunk
+ *                         sums through the per-sample buffer; same bits)
+ *   "band_samples"        samples per launch band (< 2^30): splits a render into
+ *                         more launches (same bits)
+ *   "bvh_leaf"            BVH leaf size 1, 2 or 4 at tray_scene_upload (same bits)
+ *   "bvh_lds_mode"        force LDS layout 0 / 1 / 2 when it fits (same bits)
+ *   "stack_lds_slots"     cap the traversal stack's LDS slots (overflow path; same bits)
+ *   "node_deep"           0 / 1: the 5- or 6-node-step kernel instance (same bits)
+ *   "primary_candidates"  0: camera rays traverse the BVH instead of their
+ *                         pixel's candidate list (same bits)
+ *   "resolve_staged"      0: the plain per-pixel resolve instead of the LDS-staged
+ *                         one for the ordered sum (same bits)
+ */
+#ifndef TRAY_DEBUG_H
+#define TRAY_DEBUG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Sets knob `name` to `value`. TRAY_ERR_INVALID_ARGUMENT for an unknown name. */
+int tray_debug_set(const char *name, int64_t value);
+/* Unsets knob `name`, or every knob when name is NULL. */
+int tray_debug_clear(const char *name);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRAY_DEBUG_H */

@@ -19,7 +19,39 @@ def test_exports_match_header(L):
     lib = L.lib()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.tray_abi_version() == 3  # 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get
+    assert lib.tray_abi_version() == 4  # 2: devices_progress, release_cache; 3: plan_get; 4: ORDERED_SUM flag
+
+
+def test_debug_hooks_outside_stable_header(L):
+    """include/tray_debug.h's knobs are exported but not part of tray.h's stable set."""
+    header = open(os.path.join(ROOT, "include", "tray.h")).read()
+    debug = open(os.path.join(ROOT, "include", "tray_debug.h")).read()
+    declared = set(re.findall(r"^int\s+(tray_\w+)\(", debug, re.M))
+    assert declared == set(L.DEBUG_EXPORTS)
+    assert not any(name in header for name in declared)
+    for knob in L.DEBUG_KNOBS:
+        assert f'"{knob}"' in debug
+    lib = L.lib()
+    for knob in L.DEBUG_KNOBS:
+        assert lib.tray_debug_set(knob.encode(), 1) == 0
+        assert lib.tray_debug_clear(knob.encode()) == 0
+    assert lib.tray_debug_set(b"no_such_knob", 1) == L.TRAY_ERR_INVALID_ARGUMENT
+    assert lib.tray_debug_clear(None) == 0
+    with pytest.raises(ValueError):
+        L.debug_knobs(no_such_knob=1)
+
+
+def test_library_never_reads_the_environment(L):
+    """A stray TRAY_* variable in a host process cannot change what the library
+    renders: the product .so imports no environment accessor at all (its knobs
+    are set through tray_debug_set only)."""
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--undefined-only", L.LIB_PATH], capture_output=True, text=True, check=True)
+    imported = {line.split()[-1].split("@")[0] for line in out.stdout.splitlines() if line.strip()}
+    assert not imported & {"getenv", "secure_getenv", "__secure_getenv", "environ", "__environ", "setenv"}, imported
+    assert "tray_debug_set" in subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True,
+                                              text=True, check=True).stdout
 
 
 def _setup(L, arr):

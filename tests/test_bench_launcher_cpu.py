@@ -91,3 +91,30 @@ def test_world_mismatch_is_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], capture_output=True,
                        text=True, env=env, timeout=300)
     assert r.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
+
+
+def test_profile_records_only_for_the_loaded_device_code(tmp_path):
+    """bench.py copies PMC figures (traffic, VALU issue / lane utilisation) into
+    its roofline record only when the profile was measured on the device code
+    the process loaded: a record with another code-object hash, none, or
+    another launch shape yields null with the reason."""
+    import json
+
+    import bench
+    from tray_amd import _lib
+
+    h = _lib.code_object_sha256()
+    assert h and len(h) == 64
+    rec = {"frames_per_launch": 16, "hbm_bytes_per_launch": 123, "code_object_sha256": h}
+    (tmp_path / "pmc_c2.json").write_text(json.dumps(rec))
+    got, src, why = bench._profile_json("pmc", "c2", 16, h, profiles_dir=str(tmp_path))
+    assert got == rec and why is None
+    got, src, why = bench._profile_json("pmc", "c2", 16, "0" * 64, profiles_dir=str(tmp_path))
+    assert got is None and src is None and "device code" in why
+    got, _, why = bench._profile_json("pmc", "c2", 8, h, profiles_dir=str(tmp_path))
+    assert got is None and "frames per launch" in why
+    (tmp_path / "pmc_c2.json").write_text(json.dumps({"frames_per_launch": 16, "hbm_bytes_per_launch": 1}))
+    got, _, why = bench._profile_json("pmc", "c2", 16, h, profiles_dir=str(tmp_path))
+    assert got is None and "None" in why  # records from before the hash existed are not trusted
+    got, _, why = bench._profile_json("pmc_mix", "c9", 16, h, profiles_dir=str(tmp_path))
+    assert got is None and "no pmc_mix_c9.json" in why

@@ -8,8 +8,8 @@ through the per-sample buffer. Both mechanisms give the same bits, whatever the
 order the samples finish in; against the oracle (Go's FP64 sum in sample order)
 the frames stay inside the parity bar of tests/test_gpu_parity.py (paths
 bit-exact, colour within 1e-12). Other frames keep the FP64 sum in sample order.
-The switches (TRAY_ACC_SLOTS, TRAY_FIXED_POINT) are read at every launch."""
-import contextlib
+The "acc_slots" knob (include/tray_debug.h) and TRAY_FLAG_ORDERED_SUM are read
+at every launch; the process environment is never read."""
 import os
 
 import numpy as np
@@ -23,20 +23,6 @@ pytestmark = pytest.mark.gpu
 FIXED_TOL = 2.0 ** -44  # fixed point vs the FP64 sum of the same samples: 2^-45 + the FP64 sum's own rounding
 
 
-@contextlib.contextmanager
-def env(**kv):
-    old = {k: os.environ.get(k) for k in kv}
-    os.environ.update({k: str(v) for k, v in kv.items()})
-    try:
-        yield
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
 # width/height not multiples of 8: padding pixels in the last tiles (chunks that start no sample)
 @pytest.mark.parametrize("scene,spp", [("rich2", 64), ("rich2", 128), ("dense7", 64)])
 def test_on_chip_equals_sample_buffer_and_oracle(L, O, scene, spp):
@@ -46,7 +32,7 @@ def test_on_chip_equals_sample_buffer_and_oracle(L, O, scene, spp):
     base, bseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 5)
     # per-sample buffer with integer resolve; one and two slots per wave (lanes wait for a free slot)
     for slots in (0, 1, 2, 9):
-        with env(TRAY_ACC_SLOTS=slots):
+        with L.debug_knobs(acc_slots=slots):
             rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 5)
         assert np.array_equal(seg, bseg), slots
         assert np.array_equal(rgb, base), slots
@@ -59,8 +45,7 @@ def test_fixed_point_vs_fp64_sum(L, O):
     w, h = 48, 27
     st = camera(L, RICH_SETUP, w, h)
     fixed, fseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 6)
-    with env(TRAY_FIXED_POINT=0):
-        f64, dseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 6)
+    f64, dseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 6, flags=L.FLAG_ORDERED_SUM)
     assert np.array_equal(fseg, dseg)
     err = float(np.max(np.abs(fixed - f64)))
     assert err <= FIXED_TOL, err
@@ -83,15 +68,14 @@ def test_fixed_point_formats_and_linear_scan(L, O):
 
 def test_bound_too_large_keeps_fp64_sum(L, O):
     """Albedo 3 at depth 50 bounds the colour at 3^50: no usable scale, so the
-    frame is the FP64 sum in sample order (identical to TRAY_FIXED_POINT=0)."""
+    frame is the FP64 sum in sample order (identical to TRAY_FLAG_ORDERED_SUM)."""
     sc = O.rich_scene(2).copy()
     lam = sc["material"] == 1
     sc["albedo"][lam] *= 3.0
     w, h = 24, 14
     st = camera(L, RICH_SETUP, w, h)
     a, sa = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 2)
-    with env(TRAY_FIXED_POINT=0):
-        b, sb = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 2)
+    b, sb = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 2, flags=L.FLAG_ORDERED_SUM)
     assert np.array_equal(sa, sb) and np.array_equal(a, b)
     ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, 64, 50, 0.5, 2, workers=WORKERS)
     assert np.array_equal(sa, rseg)
@@ -110,8 +94,8 @@ def test_passes_and_tiles_with_chunk_partials(L, O):
     st = camera(L, RICH_SETUP, w, h)
     dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
     try:
-        for band in (None, str(40 * 8 * spp * 3 * 2)):
-            with env(**({"TRAY_BAND_SAMPLES": band} if band else {})):
+        for band in (None, 40 * 8 * spp * 3 * 2):
+            with L.debug_knobs(band_samples=band):
                 for tiles in [{}, dict(tile_rows=2, tile_count=3, tile_index=1)]:
                     p = L.make_params(w, h, 50, spp, 0.5, 4, pass_=1, **tiles)
                     rows = L.params_rows(p)
@@ -139,8 +123,11 @@ def test_render_plan(L, O):
         try:
             p = L.make_params(w, h, depth, spp, 0.5, seed, output=L.OUT_RGB_F32)
             plans[c] = dev.plan(cam._state, p, 16).as_dict()
-            with env(TRAY_ACC_SLOTS=0):
+            with L.debug_knobs(acc_slots=0):
                 assert dev.plan(cam._state, p, 16).acc_slots == 0
+            ordered = L.make_params(w, h, depth, spp, 0.5, seed, output=L.OUT_RGB_F32, flags=L.FLAG_ORDERED_SUM)
+            op = dev.plan(cam._state, ordered, 16)
+            assert op.fixed_point_shift == 0 and op.acc_slots == 0
             lin = L.make_params(w, h, depth, spp, 0.5, seed, flags=L.FLAG_LINEAR_SCAN)
             assert dev.plan(cam._state, lin, 1).bvh == 0 and dev.plan(cam._state, lin, 1).acc_slots == 0
         finally:
@@ -152,3 +139,46 @@ def test_render_plan(L, O):
     # C2, 16 frames: one band, one 32-B record per 64 samples
     assert plans["c2"]["buffer_bytes"] == 1280 * 720 * 64 * 16 // 64 * 32
     assert plans["c2"]["lds_bytes"] <= 160 * 1024
+
+
+def test_ordered_sum_flag_vs_oracle(L, O):
+    """TRAY_FLAG_ORDERED_SUM at r = 64 (where the default is the fixed-point sum):
+    Go's FP64 colorSum in sample order (ray/tracer.go:143), so the frame matches the
+    oracle to the last bits except the attenuation product order (kernel
+    outer-first, Go inner-first): measured 99 % of channels identical."""
+    sc = O.rich_scene(2)
+    w, h = 44, 25
+    st = camera(L, RICH_SETUP, w, h)
+    rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 8, flags=L.FLAG_ORDERED_SUM)
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, 64, 50, 0.5, 8, workers=WORKERS)
+    assert np.array_equal(seg, rseg)
+    assert float(np.max(np.abs(rgb - ref))) <= 1e-15
+    assert (rgb == ref).mean() >= 0.95
+    fixed, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 8)
+    assert (fixed == ref).mean() < (rgb == ref).mean()  # the default is the fixed-point sum
+
+
+def test_environment_is_ignored(L, O):
+    """The product library reads no TRAY_* environment variable (round 3 had
+    eleven): setting the old switches changes neither the plan nor the bits."""
+    from tray_amd import ray
+
+    sc = O.rich_scene(2)
+    w, h = 40, 22
+    st = camera(L, RICH_SETUP, w, h)
+    base, bseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3)
+    dev = L.DeviceScene(ray.rich_scene_array(2, 11), ray._background(ray.DefaultBackground()), 0)
+    p = L.make_params(w, h, 50, 64, 0.5, 3)
+    plan0 = dev.plan(st, p, 1).as_dict()
+    old = dict(os.environ)
+    try:
+        os.environ.update({"TRAY_FIXED_POINT": "0", "TRAY_ACC_SLOTS": "0", "TRAY_BAND_SAMPLES": "4096",
+                           "TRAY_BVH_LDS_MODE": "0", "TRAY_PRIMARY_CANDIDATES": "0", "TRAY_NODE_DEEP": "1",
+                           "TRAY_STACK_LDS_SLOTS": "8", "TRAY_RESOLVE_STAGED": "0", "TRAY_BVH_LEAF": "4"})
+        assert dev.plan(st, p, 1).as_dict() == plan0
+        rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3)
+        assert np.array_equal(rgb, base) and np.array_equal(seg, bseg)
+    finally:
+        os.environ.clear()
+        os.environ.update(old)
+        dev.release()

@@ -6,9 +6,6 @@ samples per pixel, wide and narrow fields of view, cameras inside spheres, row
 ranges and tilings, and the cached list must follow camera and row changes.
 The traversal itself is pinned to the reference-order linear scan by
 tests/test_gpu_parity.py (test_bvh_equals_linear_scan)."""
-import contextlib
-import os
-
 import numpy as np
 import pytest
 
@@ -18,17 +15,10 @@ from test_gpu_parity import bg_struct, camera
 pytestmark = pytest.mark.gpu
 
 
-@contextlib.contextmanager
 def candidates(on: bool):
-    old = os.environ.get("TRAY_PRIMARY_CANDIDATES")
-    os.environ["TRAY_PRIMARY_CANDIDATES"] = "1" if on else "0"
-    try:
-        yield
-    finally:
-        if old is None:
-            os.environ.pop("TRAY_PRIMARY_CANDIDATES", None)
-        else:
-            os.environ["TRAY_PRIMARY_CANDIDATES"] = old
+    from tray_amd import _lib
+
+    return _lib.debug_knobs(primary_candidates=1 if on else 0)
 
 
 def both(L, spheres, setup, w, h, spp, depth, radius, seed, **kw):

@@ -81,13 +81,12 @@ def test_random_scene_vs_oracle(L, O, k):
 # backgrounds up to 12 and albedos up to 1.1 move the colour bound, so the scale
 # 2^k ranges over its limits and some cases fall back to the FP64 sum in sample
 # order (tray_render_plan_get says which). Same bar; the fixed-point frames are
-# also compared with the device's own FP64-order frames (TRAY_FIXED_POINT=0).
+# also compared with the device's own FP64-order frames (TRAY_FLAG_ORDERED_SUM).
 N_FIXED = 16
 
 
 @pytest.mark.parametrize("k", range(N_FIXED))
 def test_random_scene_fixed_point_vs_oracle(L, O, k):
-    import os
 
     rng = np.random.default_rng(5000 + k)
     n = [3, 24, 160, 600][k % 4]
@@ -111,11 +110,9 @@ def test_random_scene_fixed_point_vs_oracle(L, O, k):
     bound = float(np.abs(bg).max()) * att ** depth * 1.001
     assert (shift > 0) == (bound < 2.0 ** (47 - 44)), (k, shift, bound)
     rgb, seg = L.render(spheres, bg_struct(L, bg), st, p, 0, segments=True)
-    os.environ["TRAY_FIXED_POINT"] = "0"
-    try:
-        f64, seg2 = L.render(spheres, bg_struct(L, bg), st, p, 0, segments=True)
-    finally:
-        del os.environ["TRAY_FIXED_POINT"]
+    po = L.Params.from_buffer_copy(p)
+    po.flags |= L.FLAG_ORDERED_SUM
+    f64, seg2 = L.render(spheres, bg_struct(L, bg), st, po, 0, segments=True)
     ref, rseg = O.render(spheres, bg, st.as_array(), w, h, spp, depth, radius, seed, workers=WORKERS)
     assert np.array_equal(seg, rseg) and np.array_equal(seg2, rseg), k
     finite = np.isfinite(ref)
@@ -133,7 +130,6 @@ def test_degenerate_camera_nan_in_both_sums(L, O):
     """Up parallel to the view direction: Go's camera basis u = Unit(Cross(Up, w))
     is NaN (ray/camera.go:80), so every colour is NaN; the fixed-point sums
     (r = 64) give NaN in the same channels as the FP64 sum and the oracle."""
-    import os
 
     sc = O.rich_scene(2)
     setup = np.array([0.0, 5, 0, 0, 0, 0, 0, 1, 0, 20.0, 10.0, 10.0, 0.1])
@@ -142,10 +138,7 @@ def test_degenerate_camera_nan_in_both_sums(L, O):
     p = L.make_params(w, h, 10, 64, 0.5, 3)
     bg = np.array([1.0, 1.0, 1.0, 0.4, 0.65, 1.0])
     rgb, _ = L.render(sc, bg_struct(L, bg), st, p, 0, segments=True)
-    os.environ["TRAY_FIXED_POINT"] = "0"
-    try:
-        f64, _ = L.render(sc, bg_struct(L, bg), st, p, 0, segments=True)
-    finally:
-        del os.environ["TRAY_FIXED_POINT"]
+    f64, _ = L.render(sc, bg_struct(L, bg), st, L.make_params(w, h, 10, 64, 0.5, 3, flags=L.FLAG_ORDERED_SUM), 0,
+                      segments=True)
     ref, _ = O.render(sc, bg, st.as_array(), w, h, 64, 10, 0.5, 3, workers=WORKERS)
     assert np.array_equal(np.isfinite(rgb), np.isfinite(ref)) and np.array_equal(np.isfinite(f64), np.isfinite(ref))

@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import DEFAULT_BG, RICH_SETUP, load_golden
+from conftest import DEFAULT_BG, RICH_SETUP, SKY_EDGE_AA, SKY_EDGE_PINHOLE, load_golden, srgb_boundary_distance
 
 pytestmark = pytest.mark.gpu
 
@@ -204,6 +204,19 @@ def test_example_png_sky_rows(L, O):
     assert np.all(seg == 64)
     d = np.abs(u8[..., :3].astype(int) - rows.astype(int))
     assert d.max() <= 1 and (d.max(-1) == 0).mean() >= 0.98
+    lin, _ = gpu_render(L, sc, DEFAULT_BG, st, 1280, 720, 64, 50, 0.5, 2, y_start=0, y_end=49)
+    assert np.array_equal(O.to_srgba(lin), u8)  # the device encoder's bytes are ToSRGBA of the F64 frame
+    assert not np.any((d > 0) & (srgb_boundary_distance(lin) >= SKY_EDGE_AA))
+    # pixel-centre pinhole rays: exact bytes except within SKY_EDGE_PINHOLE of a rounding boundary
+    setup = RICH_SETUP.copy()
+    setup[12] = 0.0
+    st0 = camera(L, setup, 1280, 720)
+    lin0, seg0 = gpu_render(L, sc, DEFAULT_BG, st0, 1280, 720, 1, 50, 0.5, 2, y_start=0, y_end=49)
+    assert np.all(seg0 == 1)
+    d0 = np.abs(O.to_srgba(lin0)[..., :3].astype(int) - rows.astype(int))
+    near = srgb_boundary_distance(lin0) < SKY_EDGE_PINHOLE
+    assert d0.max() <= 1 and near.mean() < 0.03
+    assert np.array_equal(d0[~near], np.zeros_like(d0[~near]))
 
 
 def test_config2_full_size_properties(L, O):
@@ -353,20 +366,20 @@ def test_scene_info_and_traversal_paths(L, O):
                                                                 (7, 22, "1", None, 0, None), (7, 22, "4", None, 2, None),
                                                                 (7, 22, "4", "1", 2, None), (7, 22, None, None, 2, None),
                                                                 (7, 22, None, None, 2, "8"), (2, 11, "1", "2", 1, "8")])
-def test_bvh_lds_layouts(L, O, monkeypatch, seed, half, leaf, mode, resident, slots):
+def test_bvh_lds_layouts(L, O, knobs, seed, half, leaf, mode, resident, slots):
     """Every LDS layout of the BVH kernel (1: nodes + geometry; 2: nodes + leaf
     table, geometry from global memory; 0: all global), as chosen per leaf size
-    (TRAY_BVH_LEAF) or forced (TRAY_BVH_LDS_MODE), with the whole stack in LDS
+    (knob "bvh_leaf") or forced ("bvh_lds_mode"), with the whole stack in LDS
     or most of it in the overflow area, renders the linear scan's bits. The
     dense scene (1,939 spheres) picks 2-sphere leaves, nodes-only."""
     sc = O.rich_scene(seed, half)
     st = camera(L, RICH_SETUP, 48, 27)
     if leaf:
-        monkeypatch.setenv("TRAY_BVH_LEAF", leaf)
+        knobs(bvh_leaf=leaf)
     if mode:
-        monkeypatch.setenv("TRAY_BVH_LDS_MODE", mode)
+        knobs(bvh_lds_mode=mode)
     if slots:  # stack partly in the global overflow area (the spill kernels)
-        monkeypatch.setenv("TRAY_STACK_LDS_SLOTS", slots)
+        knobs(stack_lds_slots=slots)
     info = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0).info()
     assert info.has_bvh == 1 and info.lds_resident == resident
     if leaf is None:
@@ -399,13 +412,13 @@ def test_bvh_deep_tree(L, O):
     assert np.array_equal(sb, sl) and np.array_equal(bvh, lin)
 
 
-def test_launch_bands_are_invisible(L, O, monkeypatch):
-    """A frame split into several launch bands (small TRAY_BAND_SAMPLES) renders
+def test_launch_bands_are_invisible(L, O, knobs):
+    """A frame split into several launch bands (small "band_samples") renders
     the same bits as one band, tiled and untiled."""
     sc = O.rich_scene(2)
     st = camera(L, RICH_SETUP, 72, 41)
     one, s1 = gpu_render(L, sc, DEFAULT_BG, st, 72, 41, 3, 20, 0.5, 4)
-    monkeypatch.setenv("TRAY_BAND_SAMPLES", str(72 * 8 * 3 * 2))  # two 8-row tile rows per band
+    knobs(band_samples=72 * 8 * 3 * 2)  # two 8-row tile rows per band
     many, sm = gpu_render(L, sc, DEFAULT_BG, st, 72, 41, 3, 20, 0.5, 4)
     assert np.array_equal(s1, sm) and np.array_equal(one, many)
     t, stl = gpu_render(L, sc, DEFAULT_BG, st, 72, 41, 3, 20, 0.5, 4, tile_rows=8, tile_count=2, tile_index=1)
@@ -413,13 +426,13 @@ def test_launch_bands_are_invisible(L, O, monkeypatch):
     assert np.array_equal(t, one[rows]) and np.array_equal(stl, s1[rows])
 
 
-def test_stack_overflow_area(L, O, monkeypatch):
+def test_stack_overflow_area(L, O, knobs):
     """Traversal-stack slots beyond the LDS ones live in a global overflow area:
     forcing the minimum of LDS slots renders the same bits."""
     sc = O.rich_scene(2)
     st = camera(L, RICH_SETUP, 64, 36)
     a, sa = gpu_render(L, sc, DEFAULT_BG, st, 64, 36, 4, 50, 0.5, 3)
-    monkeypatch.setenv("TRAY_STACK_LDS_SLOTS", "8")
+    knobs(stack_lds_slots=8)
     b, sb = gpu_render(L, sc, DEFAULT_BG, st, 64, 36, 4, 50, 0.5, 3)
     assert np.array_equal(sa, sb) and np.array_equal(a, b)
 
@@ -447,7 +460,7 @@ def _passes(L, dev, st, p, n, dtype, shape):
 
 
 @pytest.mark.parametrize("bands", [False, True])
-def test_passes_launch_equals_single_passes(L, O, monkeypatch, bands):
+def test_passes_launch_equals_single_passes(L, O, knobs, bands):
     """tray_render_passes_async: n progressive passes in one persistent launch
     are bit-identical to n single-pass renders, in every output format, with one
     or several launch bands and with row tiles."""
@@ -457,7 +470,7 @@ def test_passes_launch_equals_single_passes(L, O, monkeypatch, bands):
     w, h, spp = 72, 41, 3
     st = camera(L, RICH_SETUP, w, h)
     if bands:
-        monkeypatch.setenv("TRAY_BAND_SAMPLES", str(72 * 8 * 3 * 3 * 2))  # two 8-row tile rows per band
+        knobs(band_samples=72 * 8 * 3 * 3 * 2)  # two 8-row tile rows per band
     dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
     try:
         for fmt, dtype, ch in [(L.OUT_RGB_F64, torch.float64, 3), (L.OUT_RGB_F32, torch.float32, 3),

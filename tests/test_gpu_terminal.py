@@ -52,3 +52,31 @@ def test_rendered_frame_to_terminal(L, O):
     assert np.array_equal(dst.cpu().numpy(), ref)
     text = terminal.ansi_halfblocks(ref)
     assert text.count("\n") == 11 and text.count("▀") == 40 * 12
+
+
+def test_scale_async_stays_in_stream_order(L, O):
+    """tray_scale_rgba_async only enqueues: it returns while a C2-sized render
+    queued before it on the same stream is still running (no host sync, no copy
+    outside the stream), and the scaled bytes are those of the finished frame."""
+    import torch
+
+    from tray_amd import ray
+
+    W, H = 1280, 720
+    cam = ray.RichSceneCamera()
+    cam.Initialize(W, H)
+    dev = L.DeviceScene(ray.rich_scene_array(2), ray._background(ray.DefaultBackground()), 0)
+    try:
+        stream = torch.cuda.Stream()
+        frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        dst = torch.zeros((24, 40, 4), dtype=torch.uint8, device="cuda")
+        p = L.make_params(W, H, 50, 64, 0.5, 2, output=L.OUT_RGBA8)
+        dev.render_async(cam._state, p, frame.data_ptr(), None, stream.cuda_stream)  # ~5 ms of work
+        L.check(L.lib().tray_scale_rgba_async(frame.data_ptr(), W, H, dst.data_ptr(), 40, 24, L.SCALE_BILINEAR, 0,
+                                              stream.cuda_stream))
+        still_running = not stream.query()
+        stream.synchronize()
+        assert still_running
+        assert np.array_equal(dst.cpu().numpy(), O.scale_rgba(frame.cpu().numpy(), 40, 24, bilinear=True))
+    finally:
+        dev.release()

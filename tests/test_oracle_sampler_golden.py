@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import DEFAULT_BG, RICH_SETUP, load_golden
+from conftest import SKY_EDGE_AA, SKY_EDGE_PINHOLE, srgb_boundary_distance, DEFAULT_BG, RICH_SETUP, load_golden
 
 
 def test_unit_vector_distribution(O):  # ray/vec3_test.go:539-649 (100k samples)
@@ -80,13 +80,20 @@ def test_example_png_sky_rows(O):
     diff = np.abs(O.to_srgba(img)[..., :3].astype(int) - rows.astype(int))
     assert diff.max() <= 1
     assert (diff.max(-1) == 0).mean() >= 0.98
-    # pixel-centre rays through a pinhole: the analytic recomputation of SURVEY.md §8(c)
+    # a 1-LSB miss only next to an encoder rounding boundary (AA noise of another stream)
+    assert not np.any((diff > 0) & (srgb_boundary_distance(img) >= SKY_EDGE_AA))
+    # pixel-centre rays through a pinhole: the analytic recomputation of SURVEY.md §8(c).
+    # No random stream is involved, so the bytes must be EXACT except where the
+    # encoded value sits within SKY_EDGE_PINHOLE of a rounding boundary.
     setup = RICH_SETUP.copy()
     setup[12] = 0.0
     _, cam0 = O.camera_initialize(setup, 1280, 720)
     img0, _ = O.render(None, DEFAULT_BG, cam0, 1280, 720, 1, 50, 0.5, 2, 0, 49)
-    d0 = np.abs(O.to_srgba(img0)[..., :3].astype(int) - rows.astype(int)).max(-1)
-    assert d0.max() <= 1 and (d0 == 0).mean() >= 0.985
+    d0 = np.abs(O.to_srgba(img0)[..., :3].astype(int) - rows.astype(int))
+    assert d0.max() <= 1 and (d0.max(-1) == 0).mean() >= 0.985
+    near = srgb_boundary_distance(img0) < SKY_EDGE_PINHOLE
+    assert near.mean() < 0.03  # the exemption covers < 3 % of channels
+    assert np.array_equal(d0[~near], np.zeros_like(d0[~near]))
 
 
 def test_oracle_workers_invariant(O):

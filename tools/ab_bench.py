@@ -5,8 +5,10 @@ and min kernel time per variant (HIP events on the launch stream).
 
     python tools/ab_bench.py [--config c2] [--rounds 5] NAME=path/libtray_amd.so[@KEY=VAL,...] ...
 
-`@KEY=VAL,...` sets environment variables for that variant's scene upload and launches
-(e.g. TRAY_BVH_LEAF_MAX, TRAY_BVH_LDS_MODE, which the library reads at those points).
+`@KEY=VAL,...` sets include/tray_debug.h knobs for that variant's scene upload and
+launches (e.g. bvh_leaf=4, bvh_lds_mode=2; a legacy TRAY_BVH_LEAF-style name maps to
+its knob). `@ordered_sum=1` renders the variant with TRAY_FLAG_ORDERED_SUM. Builds
+older than the knob API read the same settings from the environment.
 """
 import argparse
 import contextlib
@@ -30,6 +32,16 @@ def _env(env):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+def _knobs(path, kv):
+    """The variant's settings: tray_debug_set knobs, or the environment for builds that predate them."""
+    from tray_amd import _lib
+
+    names = {k.lower().removeprefix("tray_"): v for k, v in kv.items()}
+    if hasattr(_lib.lib(path), "tray_debug_set"):
+        return _lib.debug_knobs(path, **{k: int(v) for k, v in names.items()})
+    return _env({"TRAY_" + k.upper(): str(v) for k, v in names.items()})
 
 
 def main():
@@ -64,21 +76,25 @@ def main():
         name, path = v.split("=", 1)
         path, _, envs = path.partition("@")
         env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
+        ordered = int(env.pop("ordered_sum", 0))
         path = os.path.abspath(path)
-        with _env(env):
+        with _knobs(path, env):
             scene = _lib.DeviceScene(spheres, bg, 0, path)
-        runs[name] = dict(scene=scene, env=env,
+        p = _lib.Params.from_buffer_copy(params)
+        if ordered:
+            p.flags |= _lib.FLAG_ORDERED_SUM
+        runs[name] = dict(scene=scene, env=env, path=path, params=p,
                           out=torch.empty((args.passes, H, W, 3), dtype=torch.float32, device="cuda"), ms=[])
     ref = None
     for r in range(args.rounds + 1):
         for name, st in runs.items():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            with _env(st["env"]):
+            with _knobs(st["path"], st["env"]):
                 a.record(stream)
                 if args.passes == 1:
-                    st["scene"].render_async(cam._state, params, st["out"].data_ptr(), None, stream.cuda_stream)
+                    st["scene"].render_async(cam._state, st["params"], st["out"].data_ptr(), None, stream.cuda_stream)
                 else:
-                    st["scene"].render_passes_async(cam._state, params, args.passes, st["out"].data_ptr(),
+                    st["scene"].render_passes_async(cam._state, st["params"], args.passes, st["out"].data_ptr(),
                                                     stream.cuda_stream)
                 b.record(stream)
             torch.cuda.synchronize()

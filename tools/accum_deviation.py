@@ -2,7 +2,7 @@
 """Observed colour deviation of the two pixel-sum modes from the oracle (Go's FP64
 sum in sample order, oracle/tray_oracle.c), on the same seeded region of a
 benchmark scene: the fixed-point sums (default for 64 | r) and the FP64 sum in
-sample order (TRAY_FIXED_POINT=0). Prints one JSON line per config.
+sample order (TRAY_FLAG_ORDERED_SUM). Prints one JSON line per config.
 
     python tools/accum_deviation.py [--w 96 --h 54]
 """
@@ -35,9 +35,8 @@ def main():
         bg_arr = np.array(list(bg.color_a) + list(bg.color_b))
         p = L.make_params(args.w, args.h, depth, spp, 0.5, seed)
         fixed, seg = L.render(spheres, bg, cam._state, p, 0, segments=True)
-        os.environ["TRAY_FIXED_POINT"] = "0"
-        f64, seg2 = L.render(spheres, bg, cam._state, p, 0, segments=True)
-        del os.environ["TRAY_FIXED_POINT"]
+        po = L.make_params(args.w, args.h, depth, spp, 0.5, seed, flags=L.FLAG_ORDERED_SUM)
+        f64, seg2 = L.render(spheres, bg, cam._state, po, 0, segments=True)
         ref, rseg = O.render(spheres, bg_arr, cam._state.as_array(), args.w, args.h, spp, depth, 0.5, seed,
                              workers=min(16, os.cpu_count() or 4))
         print(json.dumps({

@@ -35,7 +35,11 @@ def main():
             vals.setdefault(c, []).append(v)
     counters = {c: statistics.median(v) for c, v in sorted(vals.items())}
     busy = counters.get("SQ_ACTIVE_INST_VALU")
+    hashes = {open(h).read().strip() for h in glob.glob(os.path.join(a.root, "pmc*", "code_object_sha256.txt"))}
+    if len(hashes) > 1:
+        raise SystemExit(f"counter passes measured different device code: {sorted(hashes)}")
     out = {"kernel": kernel, "label": a.label, "frames_per_launch": a.frames,
+           "code_object_sha256": hashes.pop() if hashes else None,
            "method": "tools/profile_counters.sh + profile_counters2.sh, --frames-in-flight 1, median over launches",
            "counters": counters}
     if busy and counters.get("SQ_THREAD_CYCLES_VALU"):

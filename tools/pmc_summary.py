@@ -29,6 +29,17 @@ def values(path):
     return vals[len(vals) // 3:] if len(vals) >= 3 else vals
 
 
+def code_hash(d):
+    """The device-code hash the profiling run recorded (profile_*.sh), else the in-tree build's."""
+    for p in (os.path.join(d, "code_object_sha256.txt"), os.path.join(os.path.dirname(d), "code_object_sha256.txt")):
+        if os.path.exists(p):
+            return open(p).read().strip()
+    sys.path.insert(0, ROOT)
+    from tray_amd import _lib
+
+    return _lib.code_object_sha256()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("profdir")
@@ -60,6 +71,7 @@ def main():
         shutil.copy(src, os.path.join(ROOT, "profiles", dst))
     rec = {
         "config": args.config,
+        "code_object_sha256": code_hash(d),
         "frames_per_launch": args.frames,
         "kernel": "tray::render_kernel<L, true, false, false, false, true, S> (BVH, LDS layout L, no stack spill, on-chip accumulation, S node steps)",
         "bands_per_launch": bands,

@@ -7,6 +7,8 @@ OUT=${1:-gpurun_out/pmc}; shift || true
 ARGS=${*:-"--steps 16 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
+# the device code these counters describe (bench.py only reuses them for the same code)
+python3 -c "from tray_amd import _lib; print(_lib.code_object_sha256())" > "$OUT/code_object_sha256.txt" || exit 1
 i=0
 for SET in \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU" \

@@ -6,6 +6,8 @@ OUT=${1:-gpurun_out/pmc2}; shift || true
 ARGS=${*:-"--steps 16 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
+# the device code these counters describe (bench.py only reuses them for the same code)
+python3 -c "from tray_amd import _lib; print(_lib.code_object_sha256())" > "$OUT/code_object_sha256.txt" || exit 1
 i=0
 for SET in \
   "SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_WAIT_INST_LDS SQ_INSTS_LDS" \

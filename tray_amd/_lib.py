@@ -100,6 +100,7 @@ class Params(ctypes.Structure):
 
 
 FLAG_LINEAR_SCAN = 1  # TRAY_FLAG_LINEAR_SCAN
+FLAG_ORDERED_SUM = 2  # TRAY_FLAG_ORDERED_SUM: Go's FP64 pixel sum in sample order (include/tray.h)
 
 
 class SceneInfo(ctypes.Structure):
@@ -155,6 +156,11 @@ EXPORTS = (
     "tray_to_srgba",
     "tray_linear_to_srgba_async",
 )
+
+# include/tray_debug.h: test / A-B hooks outside the stable ABI (not in EXPORTS).
+DEBUG_EXPORTS = ("tray_debug_set", "tray_debug_clear")
+DEBUG_KNOBS = ("acc_slots", "band_samples", "bvh_leaf", "bvh_lds_mode", "stack_lds_slots", "node_deep",
+               "primary_candidates", "resolve_staged")
 
 # tray_progress_fn: void (*)(int32_t rows, void *user)
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_void_p)
@@ -230,6 +236,9 @@ def lib(path: str | None = None) -> ctypes.CDLL:
     L.tray_params_rows.argtypes = [ctypes.POINTER(Params)]
     L.tray_params_rows.restype = i32
     L.tray_to_srgba.argtypes = [vp, ctypes.c_size_t, vp]
+    if hasattr(L, "tray_debug_set"):  # absent from older builds (A/B tools)
+        L.tray_debug_set.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+        L.tray_debug_clear.argtypes = [ctypes.c_char_p]
     _libs[path] = L
     return L
 
@@ -238,6 +247,78 @@ def check(rc: int) -> None:
     if rc != TRAY_OK:
         msg = lib().tray_last_error()
         raise TrayError(rc, msg.decode() if msg else "")
+
+
+_knobs_now: dict = {}  # the knobs this process has set (they are process-wide in the library)
+
+
+def set_debug_knobs(lib_path: str | None = None, **knobs) -> dict:
+    """Sets include/tray_debug.h knobs (None unsets one) and returns their
+    previous values. Test and A/B use only: the library never reads the
+    environment, so this is the one way to reach them."""
+    unknown = set(knobs) - set(DEBUG_KNOBS)
+    if unknown:
+        raise ValueError(f"unknown debug knobs {sorted(unknown)}")
+    L = lib(lib_path)
+    before = {k: _knobs_now.get(k) for k in knobs}
+    for name, value in knobs.items():
+        if value is None:
+            rc = L.tray_debug_clear(name.encode())
+            _knobs_now.pop(name, None)
+        else:
+            rc = L.tray_debug_set(name.encode(), int(value))
+            _knobs_now[name] = int(value)
+        if rc != TRAY_OK:
+            raise TrayError(rc, L.tray_last_error().decode())
+    return before
+
+
+def clear_debug_knobs(lib_path: str | None = None) -> None:
+    check(lib(lib_path).tray_debug_clear(None))
+    _knobs_now.clear()
+
+
+class debug_knobs:
+    """`with debug_knobs(acc_slots=0): ...` sets knobs for the block and restores
+    the previous values on exit."""
+
+    def __init__(self, lib_path: str | None = None, **knobs):
+        unknown = set(knobs) - set(DEBUG_KNOBS)
+        if unknown:
+            raise ValueError(f"unknown debug knobs {sorted(unknown)}")
+        self.lib_path, self.knobs, self.saved = lib_path, knobs, {}
+
+    def __enter__(self):
+        self.saved = set_debug_knobs(self.lib_path, **self.knobs)
+        return self
+
+    def __exit__(self, et, ev, tb):
+        set_debug_knobs(self.lib_path, **self.saved)
+        return False
+
+
+def code_object_sha256(path: str | None = None) -> str | None:
+    """sha256 of the device code (the ELF section .hip_fatbin: every gfx950 kernel
+    of the library) of a libtray_amd.so build. Profile records carry it
+    (tools/pmc_summary.py, tools/pmc_mix.py) so that bench.py reuses counter
+    figures only for the device code they were measured on; host-only changes
+    leave it unchanged. None when the file has no such section."""
+    import hashlib
+    import struct
+
+    with open(path or LIB_PATH, "rb") as f:
+        data = f.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:  # ELF64, little endian
+        return None
+    shoff = struct.unpack_from("<Q", data, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    names = secs[shstrndx][4]
+    for name_off, _type, _flags, _addr, off, size, *_ in secs:
+        end = data.index(b"\0", names + name_off)
+        if data[names + name_off:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()
+    return None
 
 
 def device_count() -> int:

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <deque>
@@ -19,6 +20,7 @@
 #include <vector>
 
 #include "../../include/tray.h"
+#include "../../include/tray_debug.h"
 #include "tray_internal.hpp"
 #include "bvh.hpp"
 #include "tray_kernel.hpp"
@@ -30,6 +32,25 @@ thread_local std::string g_last_error;
 int fail(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
+}
+
+// tray_debug.h knobs: a value and a set bit per knob, read at each render.
+static std::atomic<long long> g_knob_value[kKnobCount];
+static std::atomic<bool> g_knob_set[kKnobCount];
+static const char* const kKnobNames[kKnobCount] = {
+    "acc_slots", "band_samples", "bvh_leaf", "bvh_lds_mode", "stack_lds_slots", "node_deep", "primary_candidates",
+    "resolve_staged"};
+
+bool debug_knob(DebugKnob k, long long* v) {
+    if (!g_knob_set[k].load(std::memory_order_acquire)) return false;
+    *v = g_knob_value[k].load(std::memory_order_relaxed);
+    return true;
+}
+
+static int knob_index(const char* name) {
+    for (int i = 0; i < kKnobCount; ++i)
+        if (name && strcmp(name, kKnobNames[i]) == 0) return i;
+    return -1;
 }
 
 static int hip_fail(hipError_t e, const char* what) {
@@ -224,7 +245,8 @@ static int validate_params(const tray_params* p) {
         return fail(TRAY_ERR_INVALID_ARGUMENT, "tile_index must be in [0, tile_count)");
     if (p->output < TRAY_OUT_RGB_F64 || p->output > TRAY_OUT_RGBA8)
         return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown output format");
-    if (p->flags & ~TRAY_FLAG_LINEAR_SCAN) return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown flags");
+    if (p->flags & ~(TRAY_FLAG_LINEAR_SCAN | TRAY_FLAG_ORDERED_SUM))
+        return fail(TRAY_ERR_INVALID_ARGUMENT, "unknown flags");
     if (p->pass < 0) return fail(TRAY_ERR_INVALID_ARGUMENT, "pass must be >= 0");
     if (((uint64_t)p->pass + 1u) * (uint64_t)p->rays_per_pixel > 0x100000000ull)
         return fail(TRAY_ERR_TOO_LARGE, "pass x rays_per_pixel exceeds the 32-bit RNG sample word");
@@ -239,6 +261,25 @@ extern "C" {
 #pragma GCC visibility push(default)
 
 int32_t tray_abi_version(void) { return TRAY_ABI_VERSION; }
+
+int tray_debug_set(const char* name, int64_t value) {
+    const int i = knob_index(name);
+    if (i < 0) return fail(TRAY_ERR_INVALID_ARGUMENT, std::string("unknown debug knob: ") + (name ? name : "(null)"));
+    g_knob_value[i].store((long long)value, std::memory_order_relaxed);
+    g_knob_set[i].store(true, std::memory_order_release);
+    return TRAY_OK;
+}
+
+int tray_debug_clear(const char* name) {
+    if (!name) {
+        for (int i = 0; i < kKnobCount; ++i) g_knob_set[i].store(false, std::memory_order_release);
+        return TRAY_OK;
+    }
+    const int i = knob_index(name);
+    if (i < 0) return fail(TRAY_ERR_INVALID_ARGUMENT, std::string("unknown debug knob: ") + name);
+    g_knob_set[i].store(false, std::memory_order_release);
+    return TRAY_OK;
+}
 
 const char* tray_last_error(void) { return g_last_error.c_str(); }
 
@@ -313,8 +354,9 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     bool has_bvh = false;
     if (n >= kBvhMinSpheres) {
         int rank = -1, leaf_lo = 1, leaf_hi = kBvhLeafMax;
-        if (const char* e = getenv("TRAY_BVH_LEAF"))  // A/B: one leaf size only
-            leaf_lo = leaf_hi = std::max(1, std::min(kBvhLeafMax, atoi(e)));
+        long long leaf = 0;
+        if (debug_knob(kKnobBvhLeaf, &leaf))  // A/B: one leaf size only
+            leaf_lo = leaf_hi = (int)std::max(1LL, std::min((long long)kBvhLeafMax, leaf));
         for (int leaf_max = leaf_lo; leaf_max <= leaf_hi; leaf_max *= 2) {
             Bvh b;
             if (!build_bvh(spheres, n, &b, leaf_max)) continue;
@@ -448,13 +490,13 @@ int tray_scene_release(tray_scene_t sc) {
     return TRAY_OK;
 }
 
-// Primary-ray candidate lists (on unless TRAY_PRIMARY_CANDIDATES=0, an A/B and
-// test switch), for scenes whose tree has at most kCandMaxSpheres spheres (the
-// build tests every tree sphere against every 8x8 tile's beam).
+// Primary-ray candidate lists (on unless the "primary_candidates" knob is 0, an
+// A/B and test switch), for scenes whose tree has at most kCandMaxSpheres
+// spheres (the build tests every tree sphere against every 8x8 tile's beam).
 constexpr int32_t kCandMaxSpheres = 16384;
 static bool cand_enabled() {
-    const char* e = getenv("TRAY_PRIMARY_CANDIDATES");
-    return !(e && *e && atoi(e) == 0);
+    long long v = 1;
+    return !debug_knob(kKnobPrimaryCandidates, &v) || v != 0;
 }
 
 // The fixed-point scale 2^k of a render (tray_kernel.hpp), or 0 for the FP64
@@ -464,11 +506,10 @@ static bool cand_enabled() {
 // each <= max_att) times a convex combination of the two background colours,
 // so |c| <= C = max|bg| * max_att^max_depth (x 1.001 for rounding). k is the
 // largest shift with C * 2^k <= 2^kAccBits (tray_kernel.hpp).
-// TRAY_FIXED_POINT=0 forces the FP64 sum (tests, A/B).
+// TRAY_FLAG_ORDERED_SUM selects the FP64 sum in sample order (include/tray.h).
 static int32_t fixed_point_shift(const tray_scene_s* sc, const tray_params* p) {
     if (p->rays_per_pixel % 64 != 0) return 0;
-    if (const char* e = getenv("TRAY_FIXED_POINT"))
-        if (*e && atoi(e) == 0) return 0;
+    if (p->flags & TRAY_FLAG_ORDERED_SUM) return 0;
     double bg = 0.0;
     const double comps[6] = {sc->bg_a.x, sc->bg_a.y, sc->bg_a.z, sc->bg_b.x, sc->bg_b.y, sc->bg_b.z};
     for (double c : comps) {
@@ -834,7 +875,10 @@ int tray_render_progress(const tray_sphere* spheres, int32_t n, const tray_backg
     if (progress) {
         std::vector<ProgressWatch> ws{ProgressWatch{device, &sl, rows, (uint64_t)p->width * (uint64_t)p->rays_per_pixel, {}}};
         reported = poll_progress(ws, progress, user, e);
-        if (e != hipSuccess) return hip_fail(e, "render");
+        if (e != hipSuccess) {  // the launch may still write the slot's workspaces and counters
+            (void)hipStreamSynchronize(sl.stream);
+            return hip_fail(e, "render");
+        }
     }
     e = hipMemcpyAsync(out, sl.out_ws, out_bytes, hipMemcpyDeviceToHost, sl.stream);
     if (e == hipSuccess && segments_out)
@@ -998,12 +1042,13 @@ int tray_linear_to_srgba_async(const double* rgb_device, size_t n_pixels, uint8_
 
 // Frees what the synchronous entry points keep on device d (slots: cached
 // scene with its sample and candidate buffers, workspaces, streams, progress
-// counters; the sRGB table). Called with g_devices_mu held.
-static void release_device(size_t d) {
-    DeviceState* st = g_devices[d];
+// counters; the sRGB table). Lock order: a render takes st->mu and then, inside
+// (tray_scene_upload -> device_state), g_devices_mu; so this is called WITHOUT
+// g_devices_mu, on a DeviceState looked up under it (they are never deleted).
+static void release_device(DeviceState* st, int d) {
     if (!st) return;
     std::lock_guard<std::mutex> lk2(st->mu);
-    (void)hipSetDevice((int)d);
+    (void)hipSetDevice(d);
     for (Slot& sl : st->slots) {
         if (sl.stream) (void)hipStreamSynchronize(sl.stream);
         if (sl.cached) tray_scene_release(sl.cached);
@@ -1017,21 +1062,25 @@ static void release_device(size_t d) {
     st->srgb = nullptr;
 }
 
+// The device states to release (all when device < 0), copied under g_devices_mu
+// and released after dropping it (see release_device).
+static std::vector<std::pair<DeviceState*, int>> devices_to_release(int32_t device) {
+    std::vector<std::pair<DeviceState*, int>> v;
+    std::lock_guard<std::mutex> lk(g_devices_mu);
+    for (size_t d = 0; d < g_devices.size(); ++d)
+        if (g_devices[d] && (device < 0 || (size_t)device == d)) v.emplace_back(g_devices[d], (int)d);
+    return v;
+}
+
 int tray_release_cache(int32_t device) {
     if (g_in_progress_callback) return refuse_reentry("tray_release_cache");
-    std::lock_guard<std::mutex> lk(g_devices_mu);
-    if (device < 0) {
-        for (size_t d = 0; d < g_devices.size(); ++d) release_device(d);
-        return TRAY_OK;
-    }
-    if ((size_t)device < g_devices.size()) release_device((size_t)device);
+    for (auto& [st, d] : devices_to_release(device)) release_device(st, d);
     return TRAY_OK;
 }
 
 int tray_shutdown(void) {
     if (g_in_progress_callback) return refuse_reentry("tray_shutdown");
-    std::lock_guard<std::mutex> lk(g_devices_mu);
-    for (size_t d = 0; d < g_devices.size(); ++d) release_device(d);
+    for (auto& [st, d] : devices_to_release(-1)) release_device(st, d);
     return TRAY_OK;
 }
 

@@ -21,4 +21,20 @@ uint8_t srgb8(double c);
 // thresholds <= c, which is how the device encodes, bit-identical by construction.
 const double* srgb_thresholds();
 
+// Test and A/B knobs (include/tray_debug.h), set only through tray_debug_set:
+// the library never reads the process environment.
+enum DebugKnob {
+    kKnobAccSlots,
+    kKnobBandSamples,
+    kKnobBvhLeaf,
+    kKnobBvhLdsMode,
+    kKnobStackLdsSlots,
+    kKnobNodeDeep,
+    kKnobPrimaryCandidates,
+    kKnobResolveStaged,
+    kKnobCount
+};
+// True, with the value in *v, when the knob is set.
+bool debug_knob(DebugKnob k, long long* v);
+
 }  // namespace tray

@@ -35,6 +35,7 @@
 #include "bvh.hpp"
 #include "fp64.hpp"
 #include "rng.hpp"
+#include "tray_internal.hpp"
 #include "tray_kernel.hpp"
 
 namespace tray {
@@ -1928,7 +1929,8 @@ static KernelFn pick_resolve(const KernelParams& p) {
     if (p.acc_shift > 0)
         return p.acc_slots > 0 ? pick_resolve2<kResolvePartials>(p.out_format) : pick_resolve2<kResolveFixed>(p.out_format);
     bool staged = p.spp % 8 == 0;
-    if (const char* e = getenv("TRAY_RESOLVE_STAGED")) staged = staged && atoi(e) != 0;  // A/B
+    long long v = 1;
+    if (debug_knob(kKnobResolveStaged, &v)) staged = staged && v != 0;  // A/B
     return staged ? pick_resolve2<kResolveStaged>(p.out_format) : pick_resolve2<kResolveF64>(p.out_format);
 }
 
@@ -1988,11 +1990,8 @@ size_t bvh_stack_overflow_bytes(int32_t stack_cap, int device) {
 }
 
 uint64_t max_band_samples() {
-    const char* e = getenv("TRAY_BAND_SAMPLES");
-    if (e && *e) {
-        const unsigned long long v = strtoull(e, nullptr, 10);
-        if (v > 0 && v < kMaxBandSamples) return v;
-    }
+    long long v = 0;
+    if (debug_knob(kKnobBandSamples, &v) && v > 0 && (uint64_t)v < kMaxBandSamples) return (uint64_t)v;
     return kMaxBandSamples;
 }
 
@@ -2024,8 +2023,9 @@ LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
         // the nodes and leaf table when they fit, else nothing; the stack then
         // takes what LDS is left (up to its bound), the rest spills.
         L.lds_mode = bvh_lds_plan(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap).mode;
-        if (const char* m = getenv("TRAY_BVH_LDS_MODE")) {  // tests / A-B: force a layout that fits
-            const int want = atoi(m);
+        long long knob = 0;
+        if (debug_knob(kKnobBvhLdsMode, &knob)) {  // tests / A-B: force a layout that fits
+            const int want = (int)knob;
             if (want == 0 || (want == 2 && L.lds_mode != 0) ||
                 (want == 1 && bvh_scene_lds_bytes(p.n_nodes, p.n_slots, p.n_leaves, p.stack_cap) <= kMaxLDSBytes))
                 L.lds_mode = want;
@@ -2035,8 +2035,8 @@ LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
                                                : 0;
         const size_t room = kMaxLDSBytes - kUniformsBytes - scene;
         L.stack_lds = std::min<int32_t>(p.stack_cap, (int32_t)(room / kStackSlotBytes));
-        if (const char* cap = getenv("TRAY_STACK_LDS_SLOTS"))  // tests: force the overflow path
-            L.stack_lds = std::min(L.stack_lds, std::max<int32_t>(kStackLdsMin, atoi(cap)));
+        if (debug_knob(kKnobStackLdsSlots, &knob))  // tests: force the overflow path
+            L.stack_lds = std::min(L.stack_lds, (int32_t)std::max<long long>(kStackLdsMin, std::min<long long>(knob, 1 << 20)));
         L.lds = kUniformsBytes + bvh_stack_bytes(L.stack_lds) + scene;
         // Chunk accumulators in what the whole stack leaves (fixed-point frames only).
         if (p.acc_shift > 0 && L.stack_lds == p.stack_cap && p.spp % 64 == 0) {
@@ -2044,9 +2044,9 @@ LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
             const size_t per_slot = waves * kAccSlotBytes;
             const size_t left = kMaxLDSBytes - L.lds;
             int32_t slots = (int32_t)std::min<size_t>(kAccSlotsMax, left / per_slot);
-            if (const char* e = getenv("TRAY_ACC_SLOTS"))  // tests / A-B: fewer slots, 0 = off
-                slots = std::min(slots, std::max(0, atoi(e)));
-            if (slots >= kAccSlotsMin || (slots > 0 && getenv("TRAY_ACC_SLOTS"))) {
+            const bool forced = debug_knob(kKnobAccSlots, &knob);  // tests / A-B: fewer slots, 0 = off
+            if (forced) slots = (int32_t)std::min<long long>(slots, std::max(0LL, knob));
+            if (slots >= kAccSlotsMin || (slots > 0 && forced)) {
                 L.acc_slots = slots;
                 L.acc_off = (uint32_t)L.lds;
                 L.lds += (size_t)slots * per_slot;
@@ -2088,8 +2088,9 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
     bool deep = use_bvh && p.n_nodes > kDeepNodes;
-    if (const char* e = getenv("TRAY_NODE_DEEP"))  // A/B: force the instance
-        deep = use_bvh && atoi(e) != 0;
+    long long knob = 0;
+    if (debug_knob(kKnobNodeDeep, &knob))  // A/B: force the instance
+        deep = use_bvh && knob != 0;
     const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr,
                                     use_bvh && p.stack_cap > p.stack_lds, p.acc_slots > 0, deep);
     const KernelFn resolve = pick_resolve(p);

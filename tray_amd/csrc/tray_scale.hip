@@ -26,6 +26,9 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -151,6 +154,59 @@ static int hip_err(hipError_t e, const char* what) {
     return fail(TRAY_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Pinned host buffers for the tap tables, each reusable once the event recorded
+// after its last copy has fired. A handful per process (one per scale in flight).
+struct Staging {
+    void* host = nullptr;
+    size_t bytes = 0;
+    hipEvent_t done = nullptr;
+    int device = -1;
+    bool busy = false;
+};
+static std::mutex g_staging_mu;
+static std::deque<Staging> g_staging;
+
+// A buffer of >= bytes on the current device whose last copy has completed.
+static hipError_t staging_take(size_t bytes, Staging** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_staging_mu);
+    Staging* pick = nullptr;
+    for (Staging& s : g_staging) {
+        if (s.busy || s.device != dev || hipEventQuery(s.done) != hipSuccess) continue;
+        if (s.bytes >= bytes) {
+            pick = &s;
+            break;
+        }
+        if (!pick) pick = &s;  // idle but too small: grow it
+    }
+    if (!pick) {
+        g_staging.emplace_back();
+        pick = &g_staging.back();
+        pick->device = dev;
+        e = hipEventCreateWithFlags(&pick->done, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    if (pick->bytes < bytes) {
+        if (pick->host) (void)hipHostFree(pick->host);
+        pick->host = nullptr;
+        pick->bytes = 0;
+        const size_t want = std::max<size_t>(bytes, 64 << 10);
+        e = hipHostMalloc(&pick->host, want, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        pick->bytes = want;
+    }
+    pick->busy = true;
+    *out = pick;
+    return hipSuccess;
+}
+
+static void staging_give(Staging* s) {
+    std::lock_guard<std::mutex> lk(g_staging_mu);
+    s->busy = false;
+}
+
 // Enqueues the scale on `stream` (device buffers); workspace is stream-ordered.
 static int scale_enqueue(const uint8_t* src, int32_t sw, int32_t sh, uint8_t* dst, int32_t dw, int32_t dh,
                          int32_t filter, hipStream_t stream) {
@@ -180,10 +236,18 @@ static int scale_enqueue(const uint8_t* src, int32_t sw, int32_t sh, uint8_t* ds
     uint8_t* ws = nullptr;
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ws), head.size() + b_tmp, stream);
     if (e != hipSuccess) return hip_err(e, "scale workspace");
-    // The tap tables (a few KB) are staged with a synchronous copy: `head` is a
-    // local, and a pageable copy may still read it after an async call returns.
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
-    if (e == hipSuccess) e = hipMemcpy(ws, head.data(), head.size(), hipMemcpyHostToDevice);
+    // The tap tables (a few KB) go through a pinned staging buffer that stays
+    // untouched until the copy, enqueued on `stream`, has run (its event): the
+    // call neither blocks nor leaves the caller's stream order.
+    Staging* stg = nullptr;
+    e = staging_take(head.size(), &stg);
+    if (e == hipSuccess) {
+        memcpy(stg->host, head.data(), head.size());
+        e = hipMemcpyAsync(ws, stg->host, head.size(), hipMemcpyHostToDevice, stream);
+        const hipError_t r = hipEventRecord(stg->done, stream);
+        if (e == hipSuccess) e = r;
+        staging_give(stg);
+    }
     const ScaleSource* d_hs = reinterpret_cast<const ScaleSource*>(ws);
     const ScaleSource* d_vs = reinterpret_cast<const ScaleSource*>(ws + b_hs);
     const ScaleTap* d_ht = reinterpret_cast<const ScaleTap*>(ws + b_hs + b_vs);
