@@ -226,8 +226,13 @@ def main() -> int:
     if world != args.gpus:
         print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
         return 2
-    if world > 1 and backend == "nccl" and torch.cuda.device_count() < world:
-        print(f"bench.py: --gpus {world} needs {world} visible GPUs, found {torch.cuda.device_count()}",
+    ndev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and ndev == 1:
+        # A launcher that gives each rank one visible GPU (HIP_VISIBLE_DEVICES per rank):
+        # every rank renders on its device 0; distinct devices are checked below.
+        local_rank = 0
+    elif world > 1 and backend == "nccl" and ndev < world:
+        print(f"bench.py: --gpus {world} needs {world} visible GPUs (or one per rank), found {ndev}",
               file=sys.stderr)
         return 2
     torch.cuda.set_device(local_rank)
@@ -276,6 +281,13 @@ def main() -> int:
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslot - 1)]
     comm = torch.cuda.Stream() if world > 1 else None
     gathered = [None] * nslot
+    gathers = {}  # (slot, frames) -> shard.FrameGather: receive and frame buffers allocated once
+
+    def gather_for(k, n):
+        if (k, n) not in gathers:
+            gathers[(k, n)] = shard.FrameGather(n, H, W, (3,), args.tile_rows, world, rank, torch.float32,
+                                                torch.device("cuda", local_rank))
+        return gathers[(k, n)]
     scene, out, stream = scenes[0], outs[0], streams[0]
 
     def launch(k, first, n):
@@ -299,7 +311,7 @@ def main() -> int:
             if world > 1:
                 comm.wait_stream(streams[k])
                 with torch.cuda.stream(comm):
-                    shard.gather_frames(outs[k][:n], H, args.tile_rows, world, rank)
+                    gather_for(k, n)(outs[k][:n])
                     gathered[k] = torch.cuda.Event()
                     gathered[k].record(comm)
             j += 1
@@ -318,6 +330,9 @@ def main() -> int:
 
     for k in range(nslot):  # setup: each slot's sample buffer and launch state
         launch(k, 0, F)
+        if world > 1:  # and its gather buffers, for every launch size the timed frames use
+            for n in {F, args.steps % F} - {0}:
+                gather_for(k, n)
     frames(0, args.warmup)
     torch.cuda.synchronize()
     if dist:

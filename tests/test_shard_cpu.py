@@ -84,3 +84,64 @@ def test_gather_pass_batch_gloo(O, tmp_path, world, tile):
         ref = O.render(O.rich_scene(2), DEFAULT_BG, cam, W, H, SPP, DEPTH, 0.5, SEED, segments=False, pass_=k)
         assert np.array_equal(got[i], ref)
     assert not np.array_equal(got[0], got[1])
+
+
+def _old_gather(local, height, tile, world, rank):
+    """The round-3 gather (per call: padded send buffer, `world` receive buffers,
+    a fresh frame and one index_copy_ per rank), kept as the reference."""
+    import torch
+    import torch.distributed as dist
+
+    from tray_amd import shard
+
+    counts = [len(shard.rows_for(height, tile, world, r)) for r in range(world)]
+    pad = torch.zeros((local.shape[0], max(counts)) + tuple(local.shape[2:]), dtype=local.dtype)
+    pad[:, : local.shape[1]] = local
+    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+    dist.gather(pad, gather_list=bufs, dst=0)
+    if rank != 0:
+        return None
+    full = torch.empty((local.shape[0], height) + tuple(local.shape[2:]), dtype=local.dtype)
+    for r in range(world):
+        idx = torch.as_tensor(shard.rows_for(height, tile, world, r), dtype=torch.long)
+        full.index_copy_(1, idx, bufs[r][:, : counts[r]])
+    return full
+
+
+def _worker_framegather(rank, world, port, result_path):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tray_amd import shard
+
+    ok = True
+    for height, tile in [(29, 1), (29, 4), (24, 1), (31, 3), (5, 8), (90, 1)]:
+        rows = shard.rows_for(height, tile, world, rank)
+        g = shard.FrameGather(3, height, 7, (3,), tile, world, rank, torch.float32, torch.device("cpu"))
+        for call in range(3):  # the buffers are reused from call to call
+            gen = torch.Generator().manual_seed(1000 * height + 10 * tile + call)
+            frame = torch.rand((3, height, 7, 3), generator=gen)
+            local = frame[:, torch.as_tensor(rows, dtype=torch.long)].contiguous()
+            new = g(local)
+            old = _old_gather(local, height, tile, world, rank)
+            if rank == 0:
+                ok &= bool(torch.equal(new, old)) and bool(torch.equal(new, frame))
+            else:
+                ok &= new is None and old is None
+    flags = [None] * world
+    dist.all_gather_object(flags, ok)
+    if rank == 0:
+        np.save(result_path, np.array(flags))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_frame_gather_equals_round3_gather(tmp_path, world):
+    """shard.FrameGather (buffers allocated once, one strided copy into image
+    order) equals the round-3 gather bit for bit, over ragged heights, tiles with
+    a partial last tile, ranks with fewer rows than others and repeated calls."""
+    path = str(tmp_path / "ok.npy")
+    mp.spawn(_worker_framegather, args=(world, _free_port(), path), nprocs=world, join=True)
+    assert np.load(path).all()

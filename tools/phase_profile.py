@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--shard", default=None, help="N,K: rank K's row tiles of an N-way split (1-row tiles)")
     ap.add_argument("--refill-split", action="store_true", help="the library is a -DTRAY_PROFILE_REFILL build")
     ap.add_argument("--waves", type=int, default=256 * 16, help="waves in the launch (CUs x waves per CU)")
+    ap.add_argument("--material", action="store_true",
+                    help="the library is a -DTRAY_PROFILE_MATERIAL build: report the shading divergence census")
     args = ap.parse_args()
     import torch
 
@@ -39,7 +41,7 @@ def main():
         n, k = (int(v) for v in args.shard.split(","))
         params = shard.shard_params(params, 1, n, k)
     out = torch.empty((_lib.params_rows(params), W, 3), dtype=torch.float32, device="cuda")
-    stats = torch.zeros(32 + 2 * args.waves, dtype=torch.int64, device="cuda")
+    stats = torch.zeros(32 + 2 * args.waves + 64, dtype=torch.int64, device="cuda")
     scene.render_stats_async(cam._state, params, out.data_ptr(), stats.data_ptr(),
                              torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
@@ -48,7 +50,7 @@ def main():
     # -DTRAY_PROFILE_REFILL: stats[13], [16], [17], [18] (slots 10, 13-15) hold the refill split
     refill_split = dict(zip(["refill_assign", "refill_camera", "refill_hit", "refill_shade"],
                             [allv[13], allv[16], allv[17], allv[18]]))
-    se = allv[32:]
+    se = allv[32:32 + 2 * args.waves]
     names = ["segments", "sphere_tests", "box_tests", "cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade",
              "node_iters", "node_lanes", "leaf_phases", "leaf_lanes", "shade_phases", "shade_lanes", "loop_iters", "node_leafwait_lanes", "node_shadewait_lanes", "refill_phases", "refill_lanes",
              "unused_15", "rt_end_max", "rt_life_sum",
@@ -85,6 +87,19 @@ def main():
     d["waves_seen"] = int(ok.sum())
     d["wave_start_us_pct"] = {str(k): round(float(np.percentile(st_, k)) / 100.0, 1) for k in q}
     d["wave_end_us_pct"] = {str(k): round(float(np.percentile(en_, k)) / 100.0, 1) for k in q}
+    if args.material:
+        cls = ["miss", "last", "lambertian", "metal0", "metal_fuzz", "dielectric"]
+        mat = allv[32 + 2 * args.waves:]
+        for site, name in enumerate(["refill_shade", "shade"]):
+            c = mat[18 * site: 18 * site + 18]
+            passes = max(1, c[16])
+            d["material_" + name] = {
+                "passes": c[16], "lanes": c[17], "lanes_per_pass": round(c[17] / passes, 2),
+                "passes_with": {k: round(c[i] / passes, 4) for i, k in enumerate(cls)},
+                "lanes_of": {k: c[6 + i] for i, k in enumerate(cls)},
+                "lanes_per_pass_with": {k: round(c[6 + i] / max(1, c[i]), 2) for i, k in enumerate(cls)},
+                "bodies_per_pass": {str(b): round(c[12 + b] / passes, 4) for b in range(4)},
+            }
     print(json.dumps(d))
 
 

@@ -969,6 +969,25 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     return false;
 }
 
+// RayColor's last level for a segment that hit nothing: AmbientLight.Hit
+// (ray/objects.go:68-73) on its own, for the sky phase (below). The sky reads
+// only Unit(r.Direction).y: one correctly rounded quotient dir.y / |dir| (the
+// y component of unit_lsq, the same bits: Markstein's quotient is RN(a/b) in
+// range, the full division outside it), then the path ends.
+__device__ __forceinline__ double unit_y(const D3& v, double lsq) {
+    const double l = sqrt_cr(lsq);
+    bool ok = true;
+    const double q = div_rcp_nz(v.y, l, rcp_cr(l), ok);
+    return __builtin_expect(ok, 1) ? q : v.y / l;
+}
+template <bool kStats, bool kAcc>
+__device__ __forceinline__ void sky_end(const KernelParams& p, UniPtr uni, Lane& L, double dir_lsq, Stats& st,
+                                        const AccCtx& acc) {
+    const double t = 0.5 * (unit_y(L.dir, dir_lsq) + 1.0);
+    const D3 bg_a = d3(uni->bg_a.x, uni->bg_a.y, uni->bg_a.z), bg_b = d3(uni->bg_b.x, uni->bg_b.y, uni->bg_b.z);
+    end_path<kStats, kAcc>(p, L, mul(L.thr, add(smul(bg_a, 1.0 - t), smul(bg_b, t))), st, acc);
+}
+
 #ifndef TRAY_WAVES_PER_SIMD
 #define TRAY_WAVES_PER_SIMD 5
 #endif
@@ -1019,6 +1038,20 @@ constexpr int32_t kDeepNodes = 384;
 // node steps, the camera rays or the shading phase gained nothing or lost).
 #ifndef TRAY_PRIO_LEAF
 #define TRAY_PRIO_LEAF 1
+#endif
+// Sky phase: a segment that hit nothing (half the lanes of a shade phase on the book cover,
+// profiles/r6c_material_c2.json) needs only the sky colour, ~1/6 of a shading pass. With
+// TRAY_SKY_PHASE the shade phase is triggered by waiting HIT lanes (TRAY_SHADE_HIT_BATCH; the
+// misses waiting then ride along), and the misses alone are finished in a cheap sky pass once
+// TRAY_SKY_BATCH of them wait.
+#ifndef TRAY_SKY_PHASE
+#define TRAY_SKY_PHASE 0
+#endif
+#ifndef TRAY_SHADE_HIT_BATCH
+#define TRAY_SHADE_HIT_BATCH 24
+#endif
+#ifndef TRAY_SKY_BATCH
+#define TRAY_SKY_BATCH 16
 #endif
 // Camera rays answered by their candidate list are shaded inside the refill phase (1) or wait for
 // the shade phase (0).
@@ -1071,6 +1104,47 @@ constexpr int32_t kDeepNodes = 384;
 #define PROF_T0()
 #define PROF_ADD(slot)
 #define PROF_CNT(slot, v)
+#endif
+
+// Diagnostic build only (-DTRAY_PROFILE -DTRAY_PROFILE_MATERIAL): the divergence
+// census of the shading passes. Per site (0: camera-ray hits shaded in the
+// refill, 1: the shade phase) and per class of shaded lane (0 miss/sky, 1 hit at
+// the last level, 2 Lambertian, 3 Metal without fuzz, 4 Metal with fuzz, 5
+// Dielectric): [c] passes with such a lane, [6 + c] such lanes; [12 + b] passes
+// executing b of the three material bodies (b = 0..3); [16] passes, [17] lanes.
+// Added with global atomics after the per-wave stamps (stats[32 + 2 x waves + k]).
+#ifdef TRAY_PROFILE_MATERIAL
+constexpr int kMatCounters = 18;
+__device__ __forceinline__ void prof_material(int site, bool active, int32_t slot, uint32_t bounce, int32_t max_depth,
+                                              const MatRec* bmat, uint32_t lane, unsigned long long* pm) {
+    int cls = -1;
+    if (active) {
+        if (slot < 0) cls = 0;
+        else if (bounce + 1u >= (uint32_t)max_depth) cls = 1;
+        else {
+            const MatRec& m = bmat[slot];
+            cls = m.type == kLambertian ? 2 : m.type == kDielectric ? 5 : m.param > 0.0 ? 4 : 3;
+        }
+    }
+    unsigned long long* c = pm + site * kMatCounters;
+    int bodies = 0;
+    for (int k = 0; k < 6; ++k) {
+        const uint64_t m = __ballot(cls == k);
+        if (lane == 0 && m) {
+            atomicAdd(c + k, 1ull);
+            atomicAdd(c + 6 + k, (unsigned long long)__popcll(m));
+        }
+    }
+    bodies = (__ballot(cls == 2) ? 1 : 0) + (__ballot(cls == 3 || cls == 4) ? 1 : 0) + (__ballot(cls == 5) ? 1 : 0);
+    if (lane == 0) {
+        atomicAdd(c + 12 + bodies, 1ull);
+        atomicAdd(c + 16, 1ull);
+        atomicAdd(c + 17, (unsigned long long)__popcll(__ballot(active)));
+    }
+}
+#define PROF_MATERIAL(site, active) prof_material(site, active, T.slot, L.bounce, p.max_depth, p.bmat, lane, prof_mat)
+#else
+#define PROF_MATERIAL(site, active)
 #endif
 
 // Persistent megakernel: waves pull 64-pixel work items from a global counter
@@ -1201,6 +1275,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     if (lane == 0)
         for (int i = 0; i < 16; ++i) prof[i] = 0;
     const uint64_t prof_start = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef TRAY_PROFILE_MATERIAL  // counts only (global atomics: its timings are not used)
+    unsigned long long* prof_mat = p.stats + 32 + 2 * gridDim.x * (blockDim.x / 64u);
 #endif
 
     while (true) {
@@ -1347,6 +1424,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         if constexpr (kBVH) {
             if (__ballot(cam_hit) != 0ull) {
                 TRAY_MARK("refill_shade")
+                PROF_MATERIAL(0, cam_hit);
                 bool ended = false;
                 if (cam_hit) {
                     if (shade_step<kStats, kAcc>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
@@ -1492,13 +1570,34 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             }
             // Shading phase, batched.
             const uint64_t m_shade = __ballot(L.busy && T.cur == kBvhNone);
+#if TRAY_SKY_PHASE
+            const uint64_t m_sky = __ballot(L.busy && T.cur == kBvhNone && T.slot < 0);
+            const uint32_t n_hit = (uint32_t)__popcll(m_shade & ~m_sky);
+            const bool shade_now = m_shade != 0ull && (n_hit >= TRAY_SHADE_HIT_BATCH || __ballot(T.cur < kBvhNone) == 0ull ||
+                                                       (__popcll(__ballot(is_trav(T.cur))) < TRAY_TRAV_SPARSE &&
+                                                        __popcll(m_shade) >= TRAY_SHADE_LOW));
+            if (!shade_now && __popcll(m_sky) >= TRAY_SKY_BATCH) {
+                TRAY_MARK("sky")
+                PROF_T0();
+                bool ended = false;
+                if (L.busy && T.cur == kBvhNone && T.slot < 0) {
+                    sky_end<kStats, kAcc>(p, uni, L, T.a, st, acc);
+                    ended = true;
+                }
+                if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
+                PROF_ADD(3);
+            }
+            if (shade_now) {
+#else
             if (m_shade != 0ull && (__popcll(m_shade) >= TRAY_SHADE_BATCH || __ballot(T.cur < kBvhNone) == 0ull ||
                                     (__popcll(__ballot(is_trav(T.cur))) < TRAY_TRAV_SPARSE &&
                                      __popcll(m_shade) >= TRAY_SHADE_LOW))) {
+#endif
                 PROF_T0();
                 TRAY_MARK("shade_ctl")
                 PROF_CNT(8, 1);
                 PROF_CNT(9, __popcll(m_shade));
+                PROF_MATERIAL(1, L.busy && T.cur == kBvhNone);
                 bool ended = false;
                 if (L.busy && T.cur == kBvhNone) {
                     TRAY_MARK("shade")

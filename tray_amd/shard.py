@@ -47,42 +47,77 @@ def gather_frames(local, height: int, tile_rows: int, world: int, rank: int, dst
     """gather_image for a batch of frames (the passes of one
     tray_render_passes_async launch): local [n, rows_r, W, C] -> [n, height, W, C]
     on `dst`, with ONE gather for the whole batch (fewer, larger transfers over
-    xGMI)."""
-    import torch
-    import torch.distributed as dist
-
-    if local.is_cuda and dist.get_backend(group) == "gloo":
-        # gloo gathers host tensors only (RCCL, the nccl backend, gathers device
-        # memory directly over xGMI): stage through the host, hand back a device frame.
-        full = gather_frames(local.cpu(), height, tile_rows, world, rank, dst, group)
-        return None if full is None else full.to(local.device)
-    counts = [len(rows_for(height, tile_rows, world, r)) for r in range(world)]
-    max_rows = max(counts)
-    pad = local
-    if local.shape[1] < max_rows:
-        pad = torch.zeros((local.shape[0], max_rows) + tuple(local.shape[2:]), dtype=local.dtype,
-                          device=local.device)
-        pad[:, : local.shape[1]] = local
-    elif not local.is_contiguous():
-        pad = local.contiguous()
-    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
-    dist.gather(pad, gather_list=bufs, dst=dst, group=group)
-    if rank != dst:
-        return None
-    full = torch.empty((local.shape[0], height) + tuple(local.shape[2:]), dtype=local.dtype, device=local.device)
-    for r in range(world):
-        full.index_copy_(1, _row_index(height, tile_rows, world, r, local.device), bufs[r][:, : counts[r]])
-    return full
+    xGMI). The buffers are allocated once per shape (FrameGather) and the
+    returned frame is a view into one of them: it is valid until the next
+    gather of the same shape. Callers that keep several batches in flight
+    (bench.py's frame slots) hold one FrameGather each."""
+    key = (tuple(local.shape), str(local.dtype), str(local.device), height, tile_rows, world, rank, dst, id(group))
+    g = _GATHERS.get(key)
+    if g is None:
+        g = _GATHERS[key] = FrameGather(local.shape[0], height, local.shape[2], tuple(local.shape[3:]), tile_rows,
+                                        world, rank, local.dtype, local.device, dst, group)
+    return g(local)
 
 
-_ROW_INDEX = {}
+_GATHERS: dict = {}
 
 
-def _row_index(height, tile_rows, world, rank, device):
-    """Device tensor of rows_for(...), built once (no host copy per gather)."""
-    import torch
+class FrameGather:
+    """Rank `dst` assembles every rank's compact rows of F frames into image
+    order, with buffers allocated once:
 
-    key = (height, tile_rows, world, rank, str(device))
-    if key not in _ROW_INDEX:
-        _ROW_INDEX[key] = torch.as_tensor(rows_for(height, tile_rows, world, rank), dtype=torch.long, device=device)
-    return _ROW_INDEX[key]
+    * every rank sends an equal-size [F, max_rows, W, C] buffer (its own output
+      when it holds max_rows rows, else a preallocated padded copy);
+    * `dst` receives the world's buffers into ONE contiguous [world, F, max_rows,
+      W, C] tensor (the gather list is views of it);
+    * one strided copy puts them in image order: with tiles of t rows, rank k's
+      compact row i is image row (k + world * (i // t)) * t + i % t, i.e. the
+      image padded to Hpad = world * max_rows rows is
+      recv.view(world, F, max_rows / t, t, W, C) permuted to
+      (F, max_rows / t, world, t, W, C); rows >= height are padding.
+
+    This replaces a per-launch allocation of `world` receive buffers and a full
+    frame plus `world` index_copy_ scatters on `dst` (round 3), which made the
+    destination rank the straggler of every launch."""
+
+    def __init__(self, frames, height, width, channels, tile_rows, world, rank, dtype, device, dst=0, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.F, self.H, self.W, self.C = frames, height, width, tuple(channels)
+        self.t = tile_rows if tile_rows > 0 else height
+        self.world, self.rank, self.dst, self.group = world, rank, dst, group
+        self.counts = [len(rows_for(height, tile_rows, world, r)) for r in range(world)]
+        tiles = -(-height // self.t)
+        self.tiles_per_rank = -(-tiles // world)
+        self.max_rows = self.tiles_per_rank * self.t  # a multiple of t, >= every count
+        self.device = device
+        self.host_staged = str(device).startswith("cuda") and dist.get_backend(group) == "gloo"
+        buf_dev = "cpu" if self.host_staged else device
+        shape = (frames, self.max_rows, width) + self.C
+        self.send = torch.zeros(shape, dtype=dtype, device=buf_dev)
+        self.recv = self.full = None
+        if rank == dst:
+            self.recv = torch.zeros((world,) + shape, dtype=dtype, device=buf_dev)
+            self.recv_list = list(self.recv.unbind(0))
+            self.full = torch.empty((frames, world * self.max_rows, width) + self.C, dtype=dtype, device=device)
+
+    def __call__(self, local):
+        import torch.distributed as dist
+
+        n = self.counts[self.rank]
+        if tuple(local.shape) != (self.F, n, self.W) + self.C:
+            raise ValueError(f"local frames {tuple(local.shape)} != {(self.F, n, self.W) + self.C}")
+        if self.host_staged or n != self.max_rows or not local.is_contiguous():
+            self.send[:, :n].copy_(local)
+            out = self.send
+        else:
+            out = local  # already the equal-size buffer: sent as is
+        dist.gather(out, gather_list=self.recv_list if self.rank == self.dst else None, dst=self.dst,
+                    group=self.group)
+        if self.rank != self.dst:
+            return None
+        tpr, t, w = self.tiles_per_rank, self.t, self.world
+        src = self.recv.view((w, self.F, tpr, t, self.W) + self.C).permute(1, 2, 0, 3, 4, *range(5, 5 + len(self.C)))
+        self.full.view((self.F, tpr, w, t, self.W) + self.C).copy_(src)
+        return self.full[:, : self.H]
