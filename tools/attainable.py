@@ -76,7 +76,7 @@ def main():
                    "need per op of the model (CR sqrt/div, Philox, FP32 slab tests, compares/selects/moves)",
     }
     if a.phase:
-        ph = json.load(open(a.phase))
+        ph = last_json(a.phase)
         total = sum(ph[k] for k in ("cyc_refill", "cyc_node", "cyc_leaf", "cyc_shade"))
         lanes = {"cyc_refill": ph["lanes_per_refill_phase"], "cyc_node": ph["lanes_per_node_iter"],
                  "cyc_leaf": ph["lanes_per_leaf_phase"], "cyc_shade": ph["lanes_per_shade_phase"]}
