@@ -272,14 +272,7 @@ struct Lane {
 // global memory (one 32-B record per 64 samples instead of 24 B per sample)
 // and is freed; at exit the wave retires the rest. No per-sample bookkeeping.
 typedef __attribute__((address_space(3))) double LdsF64;
-// Retire a wave's freed slots in one lane-parallel pass (lane s: slot s) instead of one slot at a time.
-#ifndef TRAY_RETIRE_PARALLEL
-#define TRAY_RETIRE_PARALLEL 0
-#endif
-// With rays_per_pixel = 64 the retiring lane writes the pixel (write_chunk_pixel; needs TRAY_RETIRE_PARALLEL).
-#ifndef TRAY_FUSED_RESOLVE
-#define TRAY_FUSED_RESOLVE 0
-#endif
+
 struct AccCtx {
     LdsF64* slabs;  // this wave's slots: kAccCopies x 3 sums each
 };
@@ -407,15 +400,6 @@ __device__ __forceinline__ float f32_up(double v) {
 // leaf reference = waiting for the leaf phase; kBvhNone = traversal done,
 // waiting for the shade phase (busy lane) or idle (Lane::busy false).
 
-// Speculative traversal (Aila & Laine 2009): a lane that reaches its first leaf
-// postpones it and keeps visiting nodes, so it leaves the node steps only at its
-// second leaf (or the end of its traversal), and the leaf phase tests both. Exact
-// culling is unaffected: the closest hit only shrinks, a postponed test only
-// culls later (more node visits, never a missed sphere).
-#ifndef TRAY_SPEC_LEAF
-#define TRAY_SPEC_LEAF 0
-#endif
-
 struct Trav {
     float ix, iy, iz, oix, oiy, oiz;  // FP32 ray: t = box * inv - org * inv
     float tlim;                       // closest rounded up to float
@@ -425,9 +409,6 @@ struct Trav {
     int32_t sp;                       // stack depth (the top included)
     double a, a_inv, closest;
     int32_t slot;  // leaf slot (geometry + shading record) of the closest hit, -1: none
-#if TRAY_SPEC_LEAF
-    uint32_t pend;  // a leaf whose test is postponed while the lane keeps traversing (kBvhNone: none)
-#endif
 };
 
 // The BVH kernel runs one workgroup per CU by default (all its waves share one
@@ -523,9 +504,6 @@ __device__ __forceinline__ void trav_globals(Trav& T, const SceneView& sv, const
 // The FP32 traversal setup of a segment whose FP64 part (trav_globals) is done.
 __device__ __forceinline__ void trav_begin32(Trav& T, const SceneView& sv, const D3& org, const D3& dir) {
     T.cur = sv.n_nodes > 0 ? 0u : kBvhNone;  // the root
-#if TRAY_SPEC_LEAF
-    T.pend = kBvhNone;
-#endif
     T.sp = 0;
     T.top = ~0u;
     float dxf = (float)dir.x, dyf = (float)dir.y, dzf = (float)dir.z;
@@ -677,16 +655,6 @@ __device__ __forceinline__ void trav_node(Trav& T, const SceneView& sv, const St
     } else {
         T.cur = stack_pop(T, S, below);
     }
-#if TRAY_SPEC_LEAF
-    if (is_leaf(T.cur) && T.pend == kBvhNone) {  // postpone the first leaf, keep traversing
-        T.pend = T.cur;
-        T.cur = stack_pop(T, S, stack_load(S, max(T.sp - 1, 0)));
-    }
-    if (T.cur == kBvhNone && T.pend != kBvhNone) {  // traversal over: test the postponed leaf
-        T.cur = T.pend;
-        T.pend = kBvhNone;
-    }
-#endif
 }
 
 // The spheres of a multi-sphere leaf `ref` (FP64, any-order rule).
@@ -718,22 +686,9 @@ __device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const St
     if (sv.single) {  // one sphere per leaf: the leaf index is its slot (no leaf table, no loop)
         test_slot(T, sv, (int32_t)(T.cur & (kBvhLeafBit - 1u)), org, dir);
         tested = 1;
-#if TRAY_SPEC_LEAF
-        if (T.pend != kBvhNone) {  // the postponed leaf (speculative traversal)
-            test_slot(T, sv, (int32_t)(T.pend & (kBvhLeafBit - 1u)), org, dir);
-            T.pend = kBvhNone;
-            tested = 2;
-        }
-#endif
     } else {
         tested = 0;
         leaf_spheres(T, sv, T.cur, org, dir, tested);
-#if TRAY_SPEC_LEAF
-        if (T.pend != kBvhNone) {  // the postponed leaf (speculative traversal)
-            leaf_spheres(T, sv, T.pend, org, dir, tested);
-            T.pend = kBvhNone;
-        }
-#endif
     }
     T.tlim = f32_up(T.closest);
     T.cur = stack_pop(T, S, below);
@@ -787,10 +742,6 @@ __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni
     }
 }
 
-// TRAY_ROW_MAJOR: pixels of a band in row-major order instead of 8x8 tiles (A/B).
-#ifndef TRAY_ROW_MAJOR
-#define TRAY_ROW_MAJOR 0
-#endif
 // Work item i of a band = one sample: pixel q = i / r in 8x8-tile order of the
 // band's compact rows (so a 64-item chunk is one pixel's samples at r = 64, or
 // an 8x8 tile at r = 1), sample s = i % r.
@@ -806,18 +757,11 @@ __device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, i
         i = li;
     }
     const uint32_t q = udiv(i, p.div_spp, s);
-#if TRAY_ROW_MAJOR
-    // pixels in row-major order over the width padded to 8 (div_tiles_x divides by tiles_x * 8)
-    uint32_t xr;
-    const int32_t jb = (int32_t)udiv(q, p.div_tiles_x, xr);
-    x = (int32_t)xr;
-#else
     const uint32_t tile = q >> 6, r = q & 63u;
     uint32_t tx;
     const uint32_t ty = udiv(tile, p.div_tiles_x, tx);
     x = (int32_t)(tx * 8u + (r & 7u));
     const int32_t jb = (int32_t)(ty * 8u + (r >> 3));
-#endif
     j = p.j0 + jb;
     return x < p.width && jb < p.band_rows;
 }
@@ -925,25 +869,6 @@ __device__ __forceinline__ void write_mean(const KernelParams& p, const double* 
 // A pixel's fixed-point sums (tray_kernel.hpp): the exact integer total of its
 // r samples, converted to FP64 (one rounding) and scaled back by 2^-acc_shift
 // (exact); a channel with a NaN (non-finite) sample is NaN.
-// A 64-sample chunk that is a whole pixel of one pass (rays_per_pixel = 64):
-// its exact sums are the pixel's, so the retiring lane writes the pixel's mean
-// itself, with resolve_kernel's arithmetic (kResolvePartials: the integer sum,
-// NaN beyond 2^53, scaled by 2^-k, times 1/r): the same bits, and neither a
-// chunk record nor a resolve pass (TRAY_FUSED_RESOLVE).
-__device__ __forceinline__ void write_chunk_pixel(const KernelParams& p, uint32_t chunk, const double sum[3]) {
-    int32_t x, j;
-    uint32_t s, pass;
-    (void)decode_item(p, chunk * 64u, x, j, s, pass);  // a slot is only opened for a valid chunk
-    const double unscale = __builtin_ldexp(1.0, -p.acc_shift);
-    D3 c;
-    c.x = __builtin_fabs(sum[0]) <= 0x1p53 ? sum[0] * unscale : __builtin_nan("");
-    c.y = __builtin_fabs(sum[1]) <= 0x1p53 ? sum[1] * unscale : __builtin_nan("");
-    c.z = __builtin_fabs(sum[2]) <= 0x1p53 ? sum[2] * unscale : __builtin_nan("");
-    if (p.out_format == kOutRGBF32) write_mean<kOutRGBF32>(p, p.srgb, c, x, j, pass);
-    else if (p.out_format == kOutRGBF64) write_mean<kOutRGBF64>(p, p.srgb, c, x, j, pass);
-    else write_mean<kOutRGBA8>(p, p.srgb, c, x, j, pass);
-}
-
 // kAcc, wave-uniform: retire every open chunk (a slot in `open`) that no busy
 // lane still traces: its 64 samples have all been added, so its partial sums
 // go to global memory (record `chunk` of the launch band, kept per slot in
@@ -954,7 +879,6 @@ __device__ __forceinline__ void write_chunk_pixel(const KernelParams& p, uint32_
 __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccCtx& acc, uint64_t open, bool busy,
                                                uint32_t slot, uint32_t chunk_of, uint32_t lane) {
     uint64_t freed = 0;
-#if TRAY_RETIRE_PARALLEL
     while (open != 0ull) {
         const uint32_t s0 = (uint32_t)__builtin_ctzll(open);
         open &= open - 1ull;
@@ -972,38 +896,11 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
             for (int c = 0; c < 3; ++c) sum[c] += v[3 * k + c];
 #pragma unroll
         for (int k = 0; k < 3 * kAccCopies; ++k) v[k] = 0.0;
-        if (TRAY_FUSED_RESOLVE && p.spp == 64) {
-            write_chunk_pixel(p, chunk_of, sum);
-        } else {
-            AccPartial* o = reinterpret_cast<AccPartial*>(p.samples) + chunk_of;
-            o->sum[0] = sum[0];
-            o->sum[1] = sum[1];
-            o->sum[2] = sum[2];
-        }
+        AccPartial* o = reinterpret_cast<AccPartial*>(p.samples) + chunk_of;
+        o->sum[0] = sum[0];
+        o->sum[1] = sum[1];
+        o->sum[2] = sum[2];
     }
-#else
-    while (open != 0ull) {
-        const uint32_t s0 = (uint32_t)__builtin_ctzll(open);
-        open &= open - 1ull;
-        if (__ballot(busy && slot == s0) != 0ull) continue;
-        volatile LdsF64* v = acc.slabs + s0 * kAccCopies * 3u;
-        double sum[3] = {0.0, 0.0, 0.0};  // integers below 2^53: exact in any order
-#pragma unroll
-        for (int k = 0; k < kAccCopies; ++k)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) sum[c] += v[3 * k + c];
-        if (lane == 0u) {
-            const uint32_t chunk = __builtin_amdgcn_readlane(chunk_of, s0);
-            AccPartial* o = reinterpret_cast<AccPartial*>(p.samples) + chunk;
-            o->sum[0] = sum[0];
-            o->sum[1] = sum[1];
-            o->sum[2] = sum[2];
-#pragma unroll
-            for (int k = 0; k < 3 * kAccCopies; ++k) v[k] = 0.0;
-        }
-        freed |= 1ull << s0;
-    }
-#endif
     return freed;
 }
 
@@ -1111,25 +1008,6 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     return false;
 }
 
-// RayColor's last level for a segment that hit nothing: AmbientLight.Hit
-// (ray/objects.go:68-73) on its own, for the sky phase (below). The sky reads
-// only Unit(r.Direction).y: one correctly rounded quotient dir.y / |dir| (the
-// y component of unit_lsq, the same bits: Markstein's quotient is RN(a/b) in
-// range, the full division outside it), then the path ends.
-__device__ __forceinline__ double unit_y(const D3& v, double lsq) {
-    const double l = sqrt_cr(lsq);
-    bool ok = true;
-    const double q = div_rcp_nz(v.y, l, rcp_cr(l), ok);
-    return __builtin_expect(ok, 1) ? q : v.y / l;
-}
-template <bool kStats, bool kAcc>
-__device__ __forceinline__ void sky_end(const KernelParams& p, UniPtr uni, Lane& L, double dir_lsq, Stats& st,
-                                        const AccCtx& acc) {
-    const double t = 0.5 * (unit_y(L.dir, dir_lsq) + 1.0);
-    const D3 bg_a = d3(uni->bg_a.x, uni->bg_a.y, uni->bg_a.z), bg_b = d3(uni->bg_b.x, uni->bg_b.y, uni->bg_b.z);
-    end_path<kStats, kAcc>(p, L, mul(L.thr, add(smul(bg_a, 1.0 - t), smul(bg_b, t))), st, acc);
-}
-
 #ifndef TRAY_WAVES_PER_SIMD
 #define TRAY_WAVES_PER_SIMD 5
 #endif
@@ -1180,27 +1058,6 @@ constexpr int32_t kDeepNodes = 384;
 // node steps, the camera rays or the shading phase gained nothing or lost).
 #ifndef TRAY_PRIO_LEAF
 #define TRAY_PRIO_LEAF 1
-#endif
-// Sky phase: a segment that hit nothing (half the lanes of a shade phase on the book cover,
-// profiles/r6c_material_c2.json) needs only the sky colour, ~1/6 of a shading pass. With
-// TRAY_SKY_PHASE the shade phase is triggered by waiting HIT lanes (TRAY_SHADE_HIT_BATCH; the
-// misses waiting then ride along), and the misses alone are finished in a cheap sky pass once
-// TRAY_SKY_BATCH of them wait.
-#ifndef TRAY_SKY_PHASE
-#define TRAY_SKY_PHASE 0
-#endif
-#ifndef TRAY_SHADE_HIT_BATCH
-#define TRAY_SHADE_HIT_BATCH 24
-#endif
-#ifndef TRAY_SKY_BATCH
-#define TRAY_SKY_BATCH 16
-#endif
-#ifndef TRAY_SHADE_COUNT_MISSES
-#define TRAY_SHADE_COUNT_MISSES 0
-#endif
-// Camera-ray misses in the refill take the sky alone (sky_end) instead of the shading pass.
-#ifndef TRAY_REFILL_SKY
-#define TRAY_REFILL_SKY 0
 #endif
 // Camera rays answered by their candidate list are shaded inside the refill phase (1) or wait for
 // the shade phase (0).
@@ -1575,18 +1432,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 TRAY_MARK("refill_shade")
                 PROF_MATERIAL(0, cam_hit);
                 bool ended = false;
-#if TRAY_REFILL_SKY
-                // Camera rays that miss every sphere (sky pixels: a tenth of the refills shade
-                // nothing else) take the sky colour alone, not a whole shading pass.
-                if (cam_hit && T.slot < 0) {
-                    sky_end<kStats, kAcc>(p, uni, L, T.a, st, acc);
-                    ended = true;
-                    cam_hit = false;
-                }
-                if (__ballot(cam_hit) != 0ull && cam_hit) {
-#else
                 if (cam_hit) {
-#endif
                     if (shade_step<kStats, kAcc>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
                                                  [&] { return sv.bmat[max(T.slot, 0)]; }, st, acc)) {
                         ++L.segments;
@@ -1730,33 +1576,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             }
             // Shading phase, batched.
             const uint64_t m_shade = __ballot(L.busy && T.cur == kBvhNone);
-#if TRAY_SKY_PHASE
-            const uint64_t m_sky = __ballot(L.busy && T.cur == kBvhNone && T.slot < 0);
-#if TRAY_SHADE_COUNT_MISSES  // the shade trigger counts every waiting lane, as without the sky phase
-            const uint32_t n_hit = (uint32_t)__popcll(m_shade) >= TRAY_SHADE_BATCH ? TRAY_SHADE_HIT_BATCH : 0u;
-#else
-            const uint32_t n_hit = (uint32_t)__popcll(m_shade & ~m_sky);
-#endif
-            const bool shade_now = m_shade != 0ull && (n_hit >= TRAY_SHADE_HIT_BATCH || __ballot(T.cur < kBvhNone) == 0ull ||
-                                                       (__popcll(__ballot(is_trav(T.cur))) < TRAY_TRAV_SPARSE &&
-                                                        __popcll(m_shade) >= TRAY_SHADE_LOW));
-            if (!shade_now && __popcll(m_sky) >= TRAY_SKY_BATCH) {
-                TRAY_MARK("sky")
-                PROF_T0();
-                bool ended = false;
-                if (L.busy && T.cur == kBvhNone && T.slot < 0) {
-                    sky_end<kStats, kAcc>(p, uni, L, T.a, st, acc);
-                    ended = true;
-                }
-                if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
-                PROF_ADD(3);
-            }
-            if (shade_now) {
-#else
             if (m_shade != 0ull && (__popcll(m_shade) >= TRAY_SHADE_BATCH || __ballot(T.cur < kBvhNone) == 0ull ||
                                     (__popcll(__ballot(is_trav(T.cur))) < TRAY_TRAV_SPARSE &&
                                      __popcll(m_shade) >= TRAY_SHADE_LOW))) {
-#endif
                 PROF_T0();
                 TRAY_MARK("shade_ctl")
                 PROF_CNT(8, 1);
@@ -2304,7 +2126,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     if (p.segments && p.passes > 1) return hipErrorInvalidValue;
     p.tiles_x = (p.width + 7) / 8;
     p.div_spp = make_fastdiv((uint32_t)p.spp);
-    p.div_tiles_x = make_fastdiv((uint32_t)p.tiles_x * (TRAY_ROW_MAJOR ? 8u : 1u));
+    p.div_tiles_x = make_fastdiv((uint32_t)p.tiles_x);
     p.div_tile_rows = make_fastdiv((uint32_t)std::max(p.tile_rows, 1));
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -2326,7 +2148,6 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr,
                                     use_bvh && p.stack_cap > p.stack_lds, p.acc_slots > 0, deep);
     const KernelFn resolve = pick_resolve(p);
-    const bool fused = TRAY_FUSED_RESOLVE && TRAY_RETIRE_PARALLEL && p.acc_slots > 0 && p.spp == 64;
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {
         int dev;
@@ -2380,11 +2201,6 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         hipLaunchKernelGGL(fn, dim3(grid), dim3(threads), lds, stream, p);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
-        if (fused) {  // the megakernel wrote the pixels (write_chunk_pixel): only re-zero the queue
-            e = hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);
-            if (e != hipSuccess) return e;
-            continue;
-        }
         hipLaunchKernelGGL(resolve, dim3((pixels + 255u) / 256u, p.passes), dim3(256), 0, stream, p);
         e = hipGetLastError();
         if (e != hipSuccess) {
