@@ -468,6 +468,12 @@ def main() -> int:
             roof["valu_issue_util"] = util.get("valu_issue_utilisation")
             roof["lane_util"] = util.get("valu_lane_utilisation")
             roof["util_source"] = mix_src
+            if roof["valu_issue_util"] and roof["lane_util"]:
+                # the same instruction stream at full issue on 64 active lanes (tools/attainable.py)
+                roof["attainable"] = round(roof["frac"] / (roof["valu_issue_util"] * roof["lane_util"]), 4)
+                roof["attainable_note"] = ("frac / (valu_issue_util x lane_util): what the parity contract's "
+                                           "instruction stream allows; the rest of the gap to it is divergence "
+                                           "(1/lane_util) and issue stalls (1/valu_issue_util), DESIGN.md 8b")
         else:
             roof["valu_issue_util"] = roof["lane_util"] = None
             roof["util_null_reason"] = why_null.get("util")

@@ -31,12 +31,13 @@ def run(args):
     from tray_amd import _lib, ray, shard
 
     _, seed, half, W, H, spp, depth = CONFIGS[args.config]
+    spp = args.spp or spp
     spheres = ray.rich_scene_array(seed, half)
     cam = ray.RichSceneCamera()
     cam.Initialize(W, H)
     bg = ray._background(ray.DefaultBackground())
     base = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
-    pa = shard.shard_params(base, args.tile_rows, args.n, 0)
+    pa = shard.shard_params(base, args.tile_rows, args.n, args.rank)
     if args.force_tiles:  # the tiled code path even for n = 1 (row_of's per-item division)
         pa = _lib.Params.from_buffer_copy(base)
         pa.tile_rows, pa.tile_count, pa.tile_index = args.tile_rows, args.n, 0
@@ -59,7 +60,7 @@ def run(args):
             if r:
                 times[name].append(e0.elapsed_time(e1))
     samples = {"A": _lib.params_rows(pa) * W * spp * fa, "B": H * W * spp * fb}
-    print(json.dumps({"config": args.config, "lib": args.lib, "n": args.n, "tile_rows": args.tile_rows, "knobs": args.knob, "force_tiles": args.force_tiles, "A": {"passes": fa, "samples": samples["A"],
+    print(json.dumps({"config": args.config, "lib": args.lib, "n": args.n, "tile_rows": args.tile_rows, "knobs": args.knob, "force_tiles": args.force_tiles, "rank": args.rank, "spp": spp, "A": {"passes": fa, "samples": samples["A"],
                                                                   "median_ms": statistics.median(times["A"])},
                       "B": {"passes": fb, "samples": samples["B"], "median_ms": statistics.median(times["B"])},
                       "A_over_B_per_sample": round(statistics.median(times["A"]) / samples["A"] /
@@ -98,6 +99,8 @@ def main():
     ap.add_argument("--tile-rows", type=int, default=1)
     ap.add_argument("--lib", default=None, help="another build of libtray_amd.so (tools/build_variants.sh)")
     ap.add_argument("--force-tiles", action="store_true")
+    ap.add_argument("--rank", type=int, default=0, help="which shard A renders")
+    ap.add_argument("--spp", type=int, default=0, help="override rays per pixel")
     ap.add_argument("--knob", action="append", default=[], help="tray_debug.h knob NAME=VALUE (both A and B)")
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--summarize", nargs="*")
