@@ -93,7 +93,7 @@ struct KernelParams {
     uint32_t items;      // band work items: passes x frame_items
     uint32_t frame_items;  // one pass's items of the band: 8x8-tile-padded pixels x spp
     uint32_t passes, pass0;  // progressive passes pass0 .. pass0 + passes - 1 in this launch
-    FastDiv div_frame_items;  // item -> (pass, item within the pass)
+    FastDiv div_passes;       // (pixel x passes + pass) -> (pixel, pass): a pixel's passes are consecutive items
     size_t out_frame_bytes;  // output stride between passes
     int32_t j0, band_rows;  // the band: compact rows [j0, j0 + band_rows)
     FastDiv div_spp, div_tiles_x, div_tile_rows;  // item decoding; compact row -> image row
