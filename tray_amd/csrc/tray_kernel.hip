@@ -1031,8 +1031,10 @@ constexpr int32_t kDeepNodes = 384;
 #ifndef TRAY_LEAF_BATCH
 #define TRAY_LEAF_BATCH 20
 #endif
+// 48 since round 4's pixel-inner item order (a wave's lanes end their paths more alike): 40 / 44 /
+// 52 are +0.6 / +0.1 / +0.3 % on C2 (profiles/r6p_ab_shade_batch_c{2,5}.jsonl).
 #ifndef TRAY_SHADE_BATCH
-#define TRAY_SHADE_BATCH 40
+#define TRAY_SHADE_BATCH 48
 #endif
 // Idle lanes are refilled (a camera ray each) once this many wait, or the whole wave does.
 #ifndef TRAY_REFILL_BATCH
