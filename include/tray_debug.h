@@ -22,6 +22,9 @@
  *                         pixel's candidate list (same bits)
  *   "resolve_staged"      0: the plain per-pixel resolve instead of the LDS-staged
  *                         one for the ordered sum (same bits)
+ *   "wave_chunks"         chunks a wave reserves per work-queue take (1..64), for
+ *                         the whole launch (default: the build's size, single
+ *                         chunks near the end of the queue) (same bits)
  */
 #ifndef TRAY_DEBUG_H
 #define TRAY_DEBUG_H

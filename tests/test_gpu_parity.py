@@ -582,3 +582,35 @@ def test_concurrent_synchronous_renders(L, O):
         par = list(ex.map(run, jobs))
     for (a, sa), (b, sb) in zip(seq, par):
         assert np.array_equal(a, b) and np.array_equal(sa, sb)
+
+
+@pytest.mark.parametrize("chunks", [1, 3, 8, 64])
+def test_wave_chunk_reservations_are_invisible(L, O, knobs, chunks):
+    """Waves take 1..64 consecutive chunks per work-queue take (knob "wave_chunks",
+    forced for the whole launch, past pool ends and into the last partial pool):
+    the frames are bit-identical, for progressive passes in one launch (a pixel's
+    passes are consecutive items), row tiles and several launch bands."""
+    import torch
+
+    sc = O.rich_scene(2)
+    w, h, spp = 72, 41, 64
+    st = camera(L, RICH_SETUP, w, h)
+    dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
+    try:
+        base = {}
+        for forced in (None, chunks):
+            knobs(wave_chunks=forced, band_samples=None)
+            for tiles in [{}, dict(tile_rows=4, tile_count=3, tile_index=1)]:
+                for band in (None, 72 * 8 * spp * 3 * 2):
+                    knobs(band_samples=band)
+                    p = L.make_params(w, h, 20, spp, 0.5, 9, output=L.OUT_RGB_F32, pass_=1, **tiles)
+                    frames = _passes(L, dev, st, p, 3, torch.float32, (L.params_rows(p), w, 3))
+                    key = (str(tiles), band)
+                    if forced is None:
+                        base[key] = frames
+                    else:
+                        assert np.array_equal(frames, base[key]), (chunks, tiles, band)
+        one, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 20, 0.5, 9, output=L.OUT_RGB_F32, pass_=2)
+        assert np.array_equal(base[(str({}), None)][1], one)  # frame k of the launch = pass 1 + k rendered alone
+    finally:
+        dev.release()

@@ -32,6 +32,7 @@ enum DebugKnob {
     kKnobNodeDeep,
     kKnobPrimaryCandidates,
     kKnobResolveStaged,
+    kKnobWaveChunks,
     kKnobCount
 };
 // True, with the value in *v, when the knob is set.

@@ -715,19 +715,29 @@ constexpr uint32_t kPoolDone = 0xFFFFFFFFu;
 // exhausted. The pool word packs (end << 32) | next: one 64-bit LDS add hands
 // out `next`; the wave that finds next == end refills the pool from the global
 // queue while any other wave that overflowed waits for `end` to change.
-__device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni, uint32_t lane) {
+// A wave reserves TRAY_WAVE_CHUNKS consecutive chunks per pool take (fewer at a
+// pool's end; one each once the queue is near its end, so the launch's tail stays
+// chunk-grained): its lanes then stay on one pixel's consecutive passes for longer.
+#ifndef TRAY_WAVE_CHUNKS
+#define TRAY_WAVE_CHUNKS 1
+#endif
+__device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni, uint32_t lane, uint32_t G,
+                                               uint32_t& count) {
     typedef __attribute__((address_space(3))) uint64_t LdsU64;
     LdsU64* pool = (LdsU64*)&uni->pool;
     const volatile __attribute__((address_space(3))) uint32_t* pool_end =
         (const volatile __attribute__((address_space(3))) uint32_t*)&uni->pool + 1;
     while (true) {
         uint64_t old = 0;
-        if (lane == 0) old = __hip_atomic_fetch_add(pool, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) old = __hip_atomic_fetch_add(pool, (uint64_t)G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint32_t next = __builtin_amdgcn_readlane((uint32_t)old, 0);
         const uint32_t end = __builtin_amdgcn_readlane((uint32_t)(old >> 32), 0);
         if (end == kPoolDone) return kPoolDone;
-        if (next < end) return next;
-        if (next == end) {  // first past the end: refill
+        if (next + G <= end) {
+            count = G;
+            return next;
+        }
+        if (next <= end) {  // the take that reaches the end (exactly one per pool): refill
             uint32_t base = 0;
             const uint32_t pool_chunks = __builtin_amdgcn_readfirstlane(uni->pool_chunks);
             if (lane == 0) base = atomicAdd(p.queue, pool_chunks);
@@ -736,6 +746,10 @@ __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni
                                        ? (uint64_t)kPoolDone << 32
                                        : ((uint64_t)min(base + pool_chunks, p.nchunks) << 32) | base;
             if (lane == 0) __hip_atomic_store(pool, fresh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (next < end) {  // the pool's last chunks are this wave's
+                count = end - next;
+                return next;
+            }
             continue;
         }
         while (__builtin_amdgcn_readlane(*pool_end, 0) == end) __builtin_amdgcn_s_sleep(1);
@@ -1268,6 +1282,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     Trav T;
     T.cur = kBvhNone;  // idle
     uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: unassigned items of the current chunk
+    uint32_t grp_next = 0, grp_end = 0;    // wave-uniform: the rest of the wave's reserved chunks
+
     uint32_t pool_slot = 0;                 // kAcc, wave-uniform: the current chunk's accumulator slot
     bool exhausted = false;
 #ifdef TRAY_STATS_GROUND
@@ -1323,10 +1339,18 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         break;
                     }
                 }
-                const uint32_t c = take_chunk(p, uni, lane);
-                if (c == kPoolDone) {
-                    exhausted = true;
-                    break;
+                uint32_t c = grp_next;
+                if (grp_next < grp_end) {
+                    ++grp_next;
+                } else {
+                    uint32_t cnt = 1;
+                    c = take_chunk(p, uni, lane, grp_end >= p.late_at ? 1u : p.wave_chunks, cnt);
+                    if (c == kPoolDone) {
+                        exhausted = true;
+                        break;
+                    }
+                    grp_next = c + 1;
+                    grp_end = c + cnt;
                 }
                 pool_next = c * 64u;
                 pool_end = pool_next + 64u;
@@ -2185,6 +2209,9 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         e = hipMemsetAsync(p.segments, 0, (size_t)p.rows * (size_t)p.width * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
+    long long wave_chunks_knob = 0;
+    (void)debug_knob(kKnobWaveChunks, &wave_chunks_knob);
+    wave_chunks_knob = std::min<long long>(std::max<long long>(wave_chunks_knob, 0), 64);
     const int32_t band = band_tile_rows(p.width, spp_launch) * 8;
     const uint32_t waves = (uint32_t)threads / 64u;
     for (int32_t j0 = 0; j0 < p.rows; j0 += band) {
@@ -2196,6 +2223,15 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         p.items = p.frame_items * p.passes;
         p.nchunks = (p.items + 63u) / 64u;
         p.pool_chunks = std::min<uint32_t>(TRAY_POOL_CHUNKS, std::max<uint32_t>(16u, p.nchunks / (8u * (uint32_t)blocks)));
+        // Chunk reservations per wave (take_chunk): single chunks for the last 8 reservations'
+        // worth of every wave of the grid, so the launch's tail stays chunk-grained.
+        p.wave_chunks = std::max<uint32_t>(1u, std::min<uint32_t>(TRAY_WAVE_CHUNKS, p.pool_chunks));
+        const uint64_t late_margin = (uint64_t)p.wave_chunks * 8u * (uint64_t)blocks * waves;
+        p.late_at = p.nchunks > late_margin ? p.nchunks - (uint32_t)late_margin : 0u;
+        if (wave_chunks_knob > 0) {  // tests: this reservation size everywhere, no single-chunk tail
+            p.wave_chunks = (uint32_t)wave_chunks_knob;
+            p.late_at = p.nchunks;
+        }
         // Enough waves for every chunk, capped at what the device keeps resident.
         const uint32_t grid = std::min<uint32_t>((p.nchunks + waves - 1u) / waves, (uint32_t)blocks);
         // The queue is zero here: zeroed at allocation and by every resolve pass.

@@ -94,6 +94,8 @@ struct KernelParams {
     uint32_t frame_items;  // one pass's items of the band: 8x8-tile-padded pixels x spp
     uint32_t passes, pass0;  // progressive passes pass0 .. pass0 + passes - 1 in this launch
     FastDiv div_passes;       // (pixel x passes + pass) -> (pixel, pass): a pixel's passes are consecutive items
+    uint32_t wave_chunks;     // chunks a wave reserves per pool take (take_chunk)
+    uint32_t late_at;         // from this chunk on, single-chunk takes
     size_t out_frame_bytes;  // output stride between passes
     int32_t j0, band_rows;  // the band: compact rows [j0, j0 + band_rows)
     FastDiv div_spp, div_tiles_x, div_tile_rows;  // item decoding; compact row -> image row
