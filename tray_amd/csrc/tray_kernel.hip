@@ -719,7 +719,7 @@ constexpr uint32_t kPoolDone = 0xFFFFFFFFu;
 // pool's end; one each once the queue is near its end, so the launch's tail stays
 // chunk-grained): its lanes then stay on one pixel's consecutive passes for longer.
 #ifndef TRAY_WAVE_CHUNKS
-#define TRAY_WAVE_CHUNKS 16
+#define TRAY_WAVE_CHUNKS 32
 #endif
 __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni, uint32_t lane, uint32_t G,
                                                uint32_t& count) {
