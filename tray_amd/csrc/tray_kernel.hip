@@ -721,6 +721,10 @@ constexpr uint32_t kPoolDone = 0xFFFFFFFFu;
 #ifndef TRAY_WAVE_CHUNKS
 #define TRAY_WAVE_CHUNKS 32
 #endif
+// Single-chunk takes for the last TRAY_LATE_TAKES reservations' worth of every wave of the grid.
+#ifndef TRAY_LATE_TAKES
+#define TRAY_LATE_TAKES 8u
+#endif
 __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni, uint32_t lane, uint32_t G,
                                                uint32_t& count) {
     typedef __attribute__((address_space(3))) uint64_t LdsU64;
@@ -2226,7 +2230,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
         // Chunk reservations per wave (take_chunk): single chunks for the last 8 reservations'
         // worth of every wave of the grid, so the launch's tail stays chunk-grained.
         p.wave_chunks = std::max<uint32_t>(1u, std::min<uint32_t>(TRAY_WAVE_CHUNKS, p.pool_chunks));
-        const uint64_t late_margin = (uint64_t)p.wave_chunks * 8u * (uint64_t)blocks * waves;
+        const uint64_t late_margin = (uint64_t)p.wave_chunks * TRAY_LATE_TAKES * (uint64_t)blocks * waves;
         p.late_at = p.nchunks > late_margin ? p.nchunks - (uint32_t)late_margin : 0u;
         if (wave_chunks_knob > 0) {  // tests: this reservation size everywhere, no single-chunk tail
             p.wave_chunks = (uint32_t)wave_chunks_knob;
