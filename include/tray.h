@@ -315,11 +315,12 @@ int tray_render_async(tray_scene_t scene, const tray_camera *camera, const tray_
                       uint32_t *segments_device, void *stream);
 
 /* Consecutive progressive passes params->pass .. params->pass + n_passes - 1 of
- * the row set, as ONE persistent launch (per band): a lane that finishes its
- * last sample of pass k takes a sample of pass k + 1, so frames follow each
- * other with no per-frame tail of long paths. Frame k (bit-identical to
- * tray_render_async with pass = params->pass + k) is written at out_device +
- * k * rows * width * bytes-per-pixel. No segments output. */
+ * the row set, as ONE persistent launch (per band): the work queue holds every
+ * pass's samples (a pixel's passes consecutively, so waves trace one pixel's
+ * samples for a long run), and there is one tail of long paths per launch, not
+ * one per frame. Frame k (bit-identical to tray_render_async with pass =
+ * params->pass + k) is written at out_device + k * rows * width *
+ * bytes-per-pixel. No segments output. */
 int tray_render_passes_async(tray_scene_t scene, const tray_camera *camera, const tray_params *params,
                              int32_t n_passes, void *out_device, void *stream);
 
