@@ -202,9 +202,8 @@ def main() -> int:
                     help="launches overlap this deep (own scene copy, output and stream each): a launch's "
                          "blocks start on CUs the previous launch's last paths leave idle")
     ap.add_argument("--passes", type=int, default=16,
-                    help="at most this many frames per launch, the same at every N (tray_render_passes_async: "
-                         "consecutive progressive passes in one persistent launch, one tail of long paths per "
-                         "launch); the timed frames are split into equal launches")
+                    help="frames per launch, the same at every N (tray_render_passes_async: consecutive "
+                         "progressive passes in one persistent launch, one tail of long paths per launch)")
     ap.add_argument("--rank-timeout", type=float, default=None,
                     help="self-launched ranks (--gpus N > 1 without a launcher): stop them after this many seconds")
     args = ap.parse_args()
@@ -274,12 +273,7 @@ def main() -> int:
     # output and stream), so launch j+1 starts on the CUs launch j's last paths
     # leave idle. At N > 1 each launch's F frames are gathered to rank 0 with ONE
     # gather on a stream of its own; the next launch into the same slot waits for it.
-    # The K timed frames are split into the fewest launches of at most --passes
-    # frames, all of one size (the driver's K = 20: 2 x 10, not 16 + 4; a short
-    # last launch costs a tail of its own for few frames: 4.889 against 4.925 ms
-    # per step, profiles/r7_frames_sweep_c2.txt).
     F = max(1, min(args.passes, args.steps))
-    F = -(-args.steps // -(-args.steps // F)) if args.steps > 0 else F
     nslot = max(1, args.frames_in_flight)
     scenes = [_lib.DeviceScene(spheres, bg, local_rank) for _ in range(nslot)]
     plan = scenes[0].plan(cam._state, params, F).as_dict()  # tray_render_plan_get: how the timed launches run

@@ -1,6 +1,6 @@
 """The exact path bench.py times, checked against the oracle at its own size.
 
-bench.py (`launch`/`frames`, bench.py:275-305) renders up to 16 progressive
+bench.py (`launch`/`frames`, bench.py:275-299) renders F = 16 progressive
 passes per launch through tray_render_passes_async into TRAY_OUT_RGB_F32, with
 two frame slots (own DeviceScene - work queue, chunk records -, output and
 stream) in flight at once, and with 64 | r every pixel's samples summed on chip

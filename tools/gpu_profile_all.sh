@@ -7,7 +7,7 @@ set -u
 OUT=${1:-gpurun_out/all}
 CFG=${2:-c2}
 mkdir -p "$OUT"
-A="--config $CFG --steps 10 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"
+A="--config $CFG --steps 16 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"
 bash tools/profile_bench.sh "$OUT/bench" $A || exit 1
 bash tools/profile_counters.sh "$OUT/pmc1" $A || exit 1
 bash tools/profile_counters2.sh "$OUT/pmc2" $A || exit 1

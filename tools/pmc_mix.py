@@ -16,7 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root", help="gpu_profile_all.sh output dir (holds pmc1/, pmc2/)")
     ap.add_argument("--label", default="")
-    ap.add_argument("--frames", type=int, default=10, help="frames per launch of the profiled bench command")
+    ap.add_argument("--frames", type=int, default=16, help="frames per launch of the profiled bench command")
     a = ap.parse_args()
     vals, kernel = {}, None
     for f in sorted(glob.glob(os.path.join(a.root, "pmc*", "p*", "*counter_collection.csv"))):

@@ -45,7 +45,7 @@ def main():
     ap.add_argument("profdir")
     ap.add_argument("--config", default="c2")
     ap.add_argument("--tag", required=True)
-    ap.add_argument("--frames", type=int, default=10, help="frames per launch of the profiled bench command")
+    ap.add_argument("--frames", type=int, default=16, help="frames per launch of the profiled bench command")
     args = ap.parse_args()
     d = args.profdir
     fetch_kb = statistics.median(values(os.path.join(d, "FETCH_SIZE", "pmc_counter_collection.csv")))

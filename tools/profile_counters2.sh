@@ -3,7 +3,7 @@
 #   usage: tools/profile_counters2.sh <outdir> [bench.py args...]
 set -u
 OUT=${1:-gpurun_out/pmc2}; shift || true
-ARGS=${*:-"--steps 10 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"}
+ARGS=${*:-"--steps 16 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 # the device code these counters describe (bench.py only reuses them for the same code)
