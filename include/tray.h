@@ -184,7 +184,7 @@ int tray_shutdown(void);
  * tray_render_devices*) keep on `device` (every device when device < 0): per
  * render slot, the last uploaded scene with its sample buffer (24 B per sample
  * of a launch band: up to ~25.8 GB at 2^30 samples, e.g. a 3840x2160 r=1024
- * band) and candidate records, the output workspaces, the stream and the
+ * band; with on-chip chunk sums 32 B per 64 samples, up to 1 GB at 2^31) and candidate records, the output workspaces, the stream and the
  * progress counters. A device listed k times in one tray_render_devices call
  * keeps k slots. Long-lived callers that share the device with other users call
  * this between renders; the next synchronous render re-uploads. Scenes from

@@ -12,7 +12,8 @@
  *
  *   "acc_slots"           on-chip chunk accumulators per wave (0 = off: chunk
  *                         sums through the per-sample buffer; same bits)
- *   "band_samples"        samples per launch band (< 2^30): splits a render into
+ *   "band_samples"        samples per launch band (< 2^30; < 2^31 with on-chip
+ *                         chunk sums): splits a render into
  *                         more launches (same bits)
  *   "bvh_leaf"            BVH leaf size 1, 2 or 4 at tray_scene_upload (same bits)
  *   "bvh_lds_mode"        force LDS layout 0 / 1 / 2 when it fits (same bits)

@@ -2,7 +2,7 @@
 against the oracle pixel by pixel where the oracle can afford it.
 
 Each config's whole frame goes through tray_render_async (with its launch
-bands: C3, C4 and C5 need several 2^29-sample bands); >= 256
+bands: C3, C4 and C5 need several 2^31-sample bands); >= 256
 pixels per config are re-rendered by the oracle (ray/tracer.go:120-155
 restated): per-pixel Scene.Hit counts bit-exact, colour within 1e-12 (north-star
 gate 1e-4). The picks are biased to where paths are long (glass and metal: the
@@ -22,12 +22,13 @@ pytestmark = pytest.mark.gpu
 
 TOL, TIGHT = 1e-4, 1e-12
 WORKERS = min(16, os.cpu_count() or 4)
-MAX_BAND_SAMPLES = 1 << 30  # tray_kernel.hpp kMaxBandSamples
+MAX_BAND_SAMPLES = 1 << 30  # tray_kernel.hpp kMaxBandSamples (per-sample buffer)
+MAX_BAND_SAMPLES_ACC = 1 << 31  # kMaxBandSamplesAcc (on-chip chunk sums: the configs here)
 
 
-def band_rows(W, spp):
-    """Rows per launch band (launch_render: bands of 8-row tile rows, <= 2^29 samples)."""
-    return 8 * max(1, MAX_BAND_SAMPLES // (((W + 7) // 8) * 64 * spp))
+def band_rows(W, spp, limit=MAX_BAND_SAMPLES_ACC):
+    """Rows per launch band (launch_render: bands of 8-row tile rows, <= limit samples)."""
+    return 8 * max(1, limit // (((W + 7) // 8) * 64 * spp))
 
 
 def render_frame(L, ray, config):
@@ -59,8 +60,9 @@ def picks(seg_host, W, H, spp, rng, n_random=96, n_long=64, n_ground=64, n_band=
     chosen = rng.choice(flat, n_long, replace=False)
     xs.append(chosen % W), ys.append(chosen // W)
     xs.append(rng.integers(0, W, n_ground)), ys.append(rng.integers(int(0.6 * H), H, n_ground))
-    b = band_rows(W, spp)
-    edges = [y for k in range(b, H, b) for y in (k - 1, k)] or [0, H - 1]
+    # the rows either side of every band boundary, with and without chunk records
+    edges = sorted({y for lim in (MAX_BAND_SAMPLES_ACC, MAX_BAND_SAMPLES)
+                    for b in (band_rows(W, spp, lim),) for k in range(b, H, b) for y in (k - 1, k)}) or [0, H - 1]
     ys.append(rng.choice(np.array(edges), n_band)), xs.append(rng.integers(0, W, n_band))
     return np.concatenate(xs).astype(np.int32), np.concatenate(ys).astype(np.int32)
 
@@ -92,10 +94,11 @@ def test_config_full_frame_vs_oracle(L, O, config):
     assert err <= TOL and err <= TIGHT, err
 
 
-def test_config4_row_shards_bit_identical(L):
+def test_config4_row_shards_bit_identical(L, knobs):
     """C4 as the 8-GPU bench splits it (1-row interleaved tiles, tile k -> rank k
-    mod 8), rendered shard by shard on one device for a 64-row band spanning a
-    launch-band boundary, equals the unsharded rows bit for bit."""
+    mod 8), rendered shard by shard on one device for a 64-row window, equals the
+    unsharded rows bit for bit; the unsharded render is split into launch bands
+    of 32 rows (band_samples knob: C4's own bands, 2^31 samples, are 544 rows)."""
     import torch
 
     from bench import CONFIGS
@@ -106,12 +109,15 @@ def test_config4_row_shards_bit_identical(L):
     cam = ray.RichSceneCamera()
     cam.Initialize(W, H)
     dev = L.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0)
-    y0, y1 = 1064, 1128  # C4's launch bands are 136 rows: the band boundary 1088 lies inside
+    y0, y1 = 1064, 1128
     stream = torch.cuda.current_stream().cuda_stream
     try:
         whole = torch.empty((y1 - y0, W, 3), dtype=torch.float64, device="cuda")
+        knobs(band_samples=4 * ((W + 7) // 8) * 64 * spp)  # 4 tile rows per band: a boundary at row y0 + 32
         dev.render_async(cam._state, L.make_params(W, H, depth, spp, 0.5, seed, y_start=y0, y_end=y1),
                          whole.data_ptr(), None, stream)
+        torch.cuda.synchronize()
+        L.clear_debug_knobs()
         got = torch.zeros_like(whole)
         for k in range(8):
             p = L.make_params(W, H, depth, spp, 0.5, seed, y_start=y0, y_end=y1, tile_rows=1, tile_count=8,

@@ -50,15 +50,17 @@ def main():
     d = args.profdir
     fetch_kb = statistics.median(values(os.path.join(d, "FETCH_SIZE", "pmc_counter_collection.csv")))
     write_kb = statistics.median(values(os.path.join(d, "WRITE_SIZE", "pmc_counter_collection.csv")))
-    # A launch of F frames runs in bands of <= 2^30 samples (tray_kernel.hip band_tile_rows), one
-    # megakernel dispatch each, and the counters are per dispatch: C2 is one band per 16-frame
-    # launch, C3/C5 several.
+    # A launch of F frames runs in bands (tray_kernel.hip band_tile_rows), one megakernel
+    # dispatch each, and the counters are per dispatch: C2 is one band per 16-frame launch,
+    # C3/C5 several. With on-chip chunk sums (64 | r: every config here) a band holds up to
+    # 2^31 samples, else 2^30 (tray_kernel.hpp kMaxBandSamplesAcc / kMaxBandSamples).
     sys.path.insert(0, ROOT)
     from bench import CONFIGS
 
     _, _, _, W, H, spp, _ = CONFIGS[args.config]
     tiles_x = (W + 7) // 8
-    band_rows = 8 * max(1, (1 << 30) // (tiles_x * 64 * spp * args.frames))
+    limit = 1 << (31 if spp % 64 == 0 else 30)
+    band_rows = 8 * max(1, limit // (tiles_x * 64 * spp * args.frames))
     bands = -(-H // band_rows)
     fetch = fetch_kb * 1024 * 2 * bands
     write = write_kb * 1024 * bands

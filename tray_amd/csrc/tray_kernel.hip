@@ -2072,30 +2072,32 @@ size_t bvh_stack_overflow_bytes(int32_t stack_cap, int device) {
     return (size_t)(stack_cap - kStackLdsMin) * lanes * sizeof(uint32_t);
 }
 
-uint64_t max_band_samples() {
+uint64_t max_band_samples(bool partials) {
+    const uint64_t limit = partials ? kMaxBandSamplesAcc : kMaxBandSamples;
     long long v = 0;
-    if (debug_knob(kKnobBandSamples, &v) && v > 0 && (uint64_t)v < kMaxBandSamples) return (uint64_t)v;
-    return kMaxBandSamples;
+    if (debug_knob(kKnobBandSamples, &v) && v > 0 && (uint64_t)v < limit) return (uint64_t)v;
+    return limit;
 }
 
-// Bands of 8-row tile rows, each <= max_band_samples() samples over all of the
-// launch's passes (at least one tile row). `spp` below counts the samples of a
-// pixel in one launch: rays_per_pixel x passes.
-static int32_t band_tile_rows(int32_t width, uint64_t spp) {
+// Bands of 8-row tile rows, each <= max_band_samples(partials) samples over all of
+// the launch's passes (at least one tile row). `spp` below counts the samples of a
+// pixel in one launch: rays_per_pixel x passes. Fewer bands, fewer tails: C5's
+// 16-frame launch is 4 bands instead of 8 with chunk records.
+static int32_t band_tile_rows(int32_t width, uint64_t spp, bool partials) {
     const uint64_t per = (uint64_t)((width + 7) / 8) * 64u * spp;
-    return (int32_t)std::max<uint64_t>(1, max_band_samples() / per);
+    return (int32_t)std::max<uint64_t>(1, max_band_samples(partials) / per);
 }
 
 size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp) {
     if (rows <= 0) return 0;
-    const int32_t tile_rows = std::min(band_tile_rows(width, spp), (rows + 7) / 8);
+    const int32_t tile_rows = std::min(band_tile_rows(width, spp, false), (rows + 7) / 8);
     return (size_t)((width + 7) / 8) * 64u * (size_t)tile_rows * (size_t)spp * 3 * sizeof(double);
 }
 
 size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials) {
     if (!partials) return sample_buffer_bytes(width, rows, spp);
     if (rows <= 0) return 0;
-    const int32_t tile_rows = std::min(band_tile_rows(width, spp), (rows + 7) / 8);
+    const int32_t tile_rows = std::min(band_tile_rows(width, spp, true), (rows + 7) / 8);
     return (size_t)((width + 7) / 8) * (size_t)tile_rows * (size_t)spp * sizeof(AccPartial);  // 64 x spp / 64
 }
 
@@ -2216,7 +2218,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     long long wave_chunks_knob = 0;
     (void)debug_knob(kKnobWaveChunks, &wave_chunks_knob);
     wave_chunks_knob = std::min<long long>(std::max<long long>(wave_chunks_knob, 0), 64);
-    const int32_t band = band_tile_rows(p.width, spp_launch) * 8;
+    const int32_t band = band_tile_rows(p.width, spp_launch, p.acc_slots > 0) * 8;
     const uint32_t waves = (uint32_t)threads / 64u;
     for (int32_t j0 = 0; j0 < p.rows; j0 += band) {
         p.j0 = j0;

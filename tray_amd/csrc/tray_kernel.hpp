@@ -199,12 +199,20 @@ hipError_t launch_to_srgba(const double* rgb, size_t n_pixels, uint32_t* rgba, c
                            hipStream_t stream);
 
 // Samples per launch band (the sample buffer holds one band: 24 B per sample);
-// the TRAY_BAND_SAMPLES environment variable lowers it (tests exercise bands).
+// the band_samples debug knob (include/tray_debug.h) lowers it (tests exercise bands).
 #ifndef TRAY_BAND_LOG2
 #define TRAY_BAND_LOG2 30
 #endif
 constexpr uint64_t kMaxBandSamples = 1ull << TRAY_BAND_LOG2;  // 2^30: 25.8 GB of sample buffer (of 288 GB of HBM)
-uint64_t max_band_samples();
+// With on-chip chunk sums the buffer holds one 32-B record per 64 samples, so a band
+// is bounded by the 32-bit item indices instead: 2^31 samples (1 GB of records).
+#ifndef TRAY_BAND_LOG2_ACC
+#define TRAY_BAND_LOG2_ACC 31
+#endif
+constexpr uint64_t kMaxBandSamplesAcc = 1ull << TRAY_BAND_LOG2_ACC;
+static_assert(TRAY_BAND_LOG2_ACC <= 31, "item indices are 32-bit: a band holds at most 2^31 samples");
+// The band limit of a launch with (partials) or without on-chip chunk sums.
+uint64_t max_band_samples(bool partials = false);
 // Bytes of sample buffer launch_render needs for `rows` compact rows.
 size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp);
 // False when one 8-row band has more than 2^31 samples (item indices are 32-bit).
