@@ -655,7 +655,7 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         }
         k.cand = sc->cand;
     }
-    TRAY_HIP(launch_render(k, use_bvh, static_cast<hipStream_t>(stream)));
+    TRAY_HIP(launch_render(k, use_bvh, static_cast<hipStream_t>(stream), sc->samples_bytes));
     return TRAY_OK;
 }
 

@@ -2088,17 +2088,21 @@ static int32_t band_tile_rows(int32_t width, uint64_t spp, bool partials) {
     return (int32_t)std::max<uint64_t>(1, max_band_samples(partials) / per);
 }
 
-size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp) {
+// Bytes of the buffer one band of `band_tiles` tile rows needs: a colour per sample, or
+// one chunk record per 64 samples (partials).
+static size_t band_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials, int32_t band_tiles) {
     if (rows <= 0) return 0;
-    const int32_t tile_rows = std::min(band_tile_rows(width, spp, false), (rows + 7) / 8);
-    return (size_t)((width + 7) / 8) * 64u * (size_t)tile_rows * (size_t)spp * 3 * sizeof(double);
+    const int32_t tile_rows = std::min(band_tiles, (rows + 7) / 8);
+    const size_t samples = (size_t)((width + 7) / 8) * 64u * (size_t)tile_rows * (size_t)spp;
+    return partials ? samples / 64u * sizeof(AccPartial) : samples * 3 * sizeof(double);
+}
+
+size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp) {
+    return band_buffer_bytes(width, rows, spp, false, band_tile_rows(width, spp, false));
 }
 
 size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials) {
-    if (!partials) return sample_buffer_bytes(width, rows, spp);
-    if (rows <= 0) return 0;
-    const int32_t tile_rows = std::min(band_tile_rows(width, spp, true), (rows + 7) / 8);
-    return (size_t)((width + 7) / 8) * (size_t)tile_rows * (size_t)spp * sizeof(AccPartial);  // 64 x spp / 64
+    return band_buffer_bytes(width, rows, spp, partials, band_tile_rows(width, spp, partials));
 }
 
 LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
@@ -2149,7 +2153,7 @@ bool band_fits(int32_t width, uint64_t spp) {
     return (uint64_t)((width + 7) / 8) * 64u * spp <= 0x7FFFFFFFull;
 }
 
-hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
+hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream, size_t samples_bytes) {
     if (p.rows <= 0) return hipSuccess;
     if (p.passes < 1) p.passes = 1;
     const uint64_t spp_launch = (uint64_t)p.spp * p.passes;
@@ -2170,6 +2174,12 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     p.acc_slots = layout.acc_slots;
     p.acc_off = layout.acc_off;
     if (use_bvh && p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
+    // The caller sized p.samples for this layout and band limit; both read debug knobs
+    // (tray_debug.h), so a knob changed in between must not let a band overrun it: the
+    // band is read once here and checked against the buffer.
+    const int32_t band_tiles = band_tile_rows(p.width, spp_launch, p.acc_slots > 0);
+    if (band_buffer_bytes(p.width, p.rows, spp_launch, p.acc_slots > 0, band_tiles) > samples_bytes)
+        return hipErrorInvalidValue;
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
     bool deep = use_bvh && p.n_nodes > kDeepNodes;
@@ -2218,7 +2228,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream) {
     long long wave_chunks_knob = 0;
     (void)debug_knob(kKnobWaveChunks, &wave_chunks_knob);
     wave_chunks_knob = std::min<long long>(std::max<long long>(wave_chunks_knob, 0), 64);
-    const int32_t band = band_tile_rows(p.width, spp_launch, p.acc_slots > 0) * 8;
+    const int32_t band = band_tiles * 8;
     const uint32_t waves = (uint32_t)threads / 64u;
     for (int32_t j0 = 0; j0 < p.rows; j0 += band) {
         p.j0 = j0;

@@ -134,7 +134,9 @@ struct KernelParams {
     const uint4* cand;   // nullable (BVH only): primary-ray candidate record per compact pixel (launch_cand_build)
 };
 
-hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream);
+// `samples_bytes`: the capacity of p.samples; a launch whose bands need more is refused
+// (hipErrorInvalidValue) before anything is enqueued.
+hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream, size_t samples_bytes);
 
 // Fixed-point accumulation. A sample's colour c (already scaled by 2^k through
 // the background) is rounded to the integer v = rint(c), |v| <= 2^kAccBits; any
