@@ -80,3 +80,13 @@ def test_scale_async_stays_in_stream_order(L, O):
         assert np.array_equal(dst.cpu().numpy(), O.scale_rgba(frame.cpu().numpy(), 40, 24, bilinear=True))
     finally:
         dev.release()
+
+
+def test_scale_after_shutdown(L, O):
+    """tray_shutdown frees the scaler's pinned staging buffers too; the next
+    scale allocates new ones and gives the same bytes."""
+    img = rgba(45, 80, seed=11, opaque=False)
+    ref = O.scale_rgba(img, 30, 17, bilinear=True)
+    assert np.array_equal(L.scale_rgba(img, 30, 17, bilinear=True), ref)
+    L.check(L.lib().tray_shutdown())
+    assert np.array_equal(L.scale_rgba(img, 30, 17, bilinear=True), ref)

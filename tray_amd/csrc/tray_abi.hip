@@ -1081,6 +1081,7 @@ int tray_release_cache(int32_t device) {
 int tray_shutdown(void) {
     if (g_in_progress_callback) return refuse_reentry("tray_shutdown");
     for (auto& [st, d] : devices_to_release(-1)) release_device(st, d);
+    scale_release_staging();
     return TRAY_OK;
 }
 

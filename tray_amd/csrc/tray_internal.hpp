@@ -38,4 +38,8 @@ enum DebugKnob {
 // True, with the value in *v, when the knob is set.
 bool debug_knob(DebugKnob k, long long* v);
 
+// tray_scale.hip: free the pinned tap-table staging buffers whose copies have
+// completed (tray_shutdown).
+void scale_release_staging();
+
 }  // namespace tray

@@ -207,6 +207,19 @@ static void staging_give(Staging* s) {
     s->busy = false;
 }
 
+void scale_release_staging() {
+    std::lock_guard<std::mutex> lk(g_staging_mu);
+    for (auto it = g_staging.begin(); it != g_staging.end();) {
+        if (it->busy || (it->done && hipEventSynchronize(it->done) != hipSuccess)) {
+            ++it;  // in use by a concurrent call, or its device failed: left as is
+            continue;
+        }
+        if (it->host) (void)hipHostFree(it->host);
+        if (it->done) (void)hipEventDestroy(it->done);
+        it = g_staging.erase(it);
+    }
+}
+
 // Enqueues the scale on `stream` (device buffers); workspace is stream-ordered.
 static int scale_enqueue(const uint8_t* src, int32_t sw, int32_t sh, uint8_t* dst, int32_t dw, int32_t dh,
                          int32_t filter, hipStream_t stream) {
