@@ -18,7 +18,11 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = ", true, false, false, false, true, "  # the timed BVH kernel (on-chip accumulation), any LDS layout (1: book cover, 2: dense C5) and step count
+# The timed BVH kernel, any LDS layout (1: book cover, 2: dense C5) and step count:
+# render_kernel<L, bvh, stats, progress, spill, on-chip accumulation, S>. The accumulation
+# instance runs when 64 | r (C2-C5); C1 (r = 16) sums through the per-sample buffer.
+KERNELS = {True: ", true, false, false, false, true, ", False: ", true, false, false, false, false, "}
+KERNEL = KERNELS[True]
 
 
 def values(path):
@@ -41,6 +45,7 @@ def code_hash(d):
 
 
 def main():
+    global KERNEL
     ap = argparse.ArgumentParser()
     ap.add_argument("profdir")
     ap.add_argument("--config", default="c2")
@@ -48,11 +53,9 @@ def main():
     ap.add_argument("--frames", type=int, default=16, help="frames per launch of the profiled bench command")
     args = ap.parse_args()
     d = args.profdir
-    fetch_kb = statistics.median(values(os.path.join(d, "FETCH_SIZE", "pmc_counter_collection.csv")))
-    write_kb = statistics.median(values(os.path.join(d, "WRITE_SIZE", "pmc_counter_collection.csv")))
     # A launch of F frames runs in bands (tray_kernel.hip band_tile_rows), one megakernel
     # dispatch each, and the counters are per dispatch: C2 is one band per 16-frame launch,
-    # C3/C5 several. With on-chip chunk sums (64 | r: every config here) a band holds up to
+    # C3/C5 several. With on-chip chunk sums (64 | r: C2-C5) a band holds up to
     # 2^31 samples, else 2^30 (tray_kernel.hpp kMaxBandSamplesAcc / kMaxBandSamples).
     sys.path.insert(0, ROOT)
     from bench import CONFIGS
@@ -60,6 +63,9 @@ def main():
     _, _, _, W, H, spp, _ = CONFIGS[args.config]
     tiles_x = (W + 7) // 8
     limit = 1 << (31 if spp % 64 == 0 else 30)
+    KERNEL = KERNELS[spp % 64 == 0]
+    fetch_kb = statistics.median(values(os.path.join(d, "FETCH_SIZE", "pmc_counter_collection.csv")))
+    write_kb = statistics.median(values(os.path.join(d, "WRITE_SIZE", "pmc_counter_collection.csv")))
     band_rows = 8 * max(1, limit // (tiles_x * 64 * spp * args.frames))
     bands = -(-H // band_rows)
     fetch = fetch_kb * 1024 * 2 * bands
@@ -75,7 +81,8 @@ def main():
         "config": args.config,
         "code_object_sha256": code_hash(d),
         "frames_per_launch": args.frames,
-        "kernel": "tray::render_kernel<L, true, false, false, false, true, S> (BVH, LDS layout L, no stack spill, on-chip accumulation, S node steps)",
+        "kernel": f"tray::render_kernel<L, true, false, false, false, {str(spp % 64 == 0).lower()}, S> (BVH, LDS layout L, "
+                  f"no stack spill, {'on-chip accumulation' if spp % 64 == 0 else 'per-sample buffer'}, S node steps)",
         "bands_per_launch": bands,
         "FETCH_SIZE_KB_raw_per_dispatch": fetch_kb,
         "WRITE_SIZE_KB_per_dispatch": write_kb,
