@@ -178,7 +178,8 @@ int32_t tray_abi_version(void);
 const char *tray_last_error(void);
 /* Number of usable gfx950 devices (0 when none). */
 int tray_device_count(int32_t *count);
-/* Free every library-owned device buffer on every device. */
+/* Free every library-owned device buffer on every device, and the pinned host
+ * buffers tray_scale_rgba* staged its tap tables in. */
 int tray_shutdown(void);
 /* Free what the synchronous entry points (tray_render, tray_render_progress,
  * tray_render_devices*) keep on `device` (every device when device < 0): per
