@@ -56,7 +56,19 @@ Also reported (rank 0):
                rt.Render), cold (BVH build, upload, allocation) and warm.
   cpu_baseline the oracle (C port of the reference's CPU loop with the
                reference's chunk-queue scheduler, ray/tracer.go:86-116) timed on
-               a bounded row sample of the same frame on the host cores.
+               a bounded row sample of the same frame on the host cores (frames
+               smaller than --cpu-min-seconds of work, C1, are rendered as
+               several progressive passes until that much time has passed).
+  parity       the per-pixel L-inf of the metric: pass 0 of the frame rendered
+               on the device (untimed) against the oracle's render of the same
+               pass that cpu_baseline produced, over every pixel of the rows the
+               oracle rendered (the whole frame at C1/C2; every k-th row at
+               C3/C5): the FP64 output (tray_render_async, TRAY_OUT_RGB_F64) and
+               frame 0 of a passes launch in the timed shape (TRAY_OUT_RGB_F32),
+               plus the per-pixel Scene.Hit counts (bit-exact). Gate 1e-4.
+  ranks        (N > 1) each rank's render time per frame (HIP events, one
+               launch of F frames of its rows) and one gather of F frames, so
+               a measured curve separates imbalance from the gather.
 """
 from __future__ import annotations
 
@@ -165,7 +177,9 @@ def launch_ranks(n: int, argv: list, timeout: float | None = None, script: str |
                 for q in live:
                     q.terminate()
         if deadline is not None and time.monotonic() > deadline and live:
-            print(f"bench.py: ranks timed out after {timeout} s", file=sys.stderr)
+            stuck = sorted(procs.index(q) for q in live)
+            print(f"bench.py: rank(s) {stuck} still running after {timeout} s (--rank-timeout): stopping them",
+                  file=sys.stderr)
             for q in live:
                 q.kill()
             rc = rc or 124
@@ -204,14 +218,18 @@ def main() -> int:
     ap.add_argument("--passes", type=int, default=16,
                     help="frames per launch, the same at every N (tray_render_passes_async: consecutive "
                          "progressive passes in one persistent launch, one tail of long paths per launch)")
-    ap.add_argument("--rank-timeout", type=float, default=None,
-                    help="self-launched ranks (--gpus N > 1 without a launcher): stop them after this many seconds")
+    ap.add_argument("--rank-timeout", type=float, default=900.0,
+                    help="self-launched ranks (--gpus N > 1 without a launcher): stop them after this many seconds "
+                         "and exit non-zero, naming the ranks still running (0: no limit)")
+    ap.add_argument("--cpu-min-seconds", type=float, default=10.0,
+                    help="cpu_baseline: render further progressive passes of the sample until this much time has "
+                         "passed (small frames, C1)")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # No launcher: start the N ranks here, before anything touches the GPU.
-        return launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout)
+        return launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout if args.rank_timeout > 0 else None)
 
     import torch
 
@@ -358,10 +376,33 @@ def main() -> int:
 
     kernel_ms = launch_ms(F)  # the timed launch shape: F frames, megakernel + F resolves
     single_ms = kernel_ms if F == 1 else None if args.no_single else launch_ms(1)  # one frame, nothing overlapped
+    ranks_rec = None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # Untimed, per rank: the render of its rows (kernel_ms above) and one gather of F frames
+        # (HIP events on the gather's stream), so a measured curve separates imbalance from the gather.
+        torch.cuda.synchronize()
+        dist.barrier()
+        g = gather_for(0, F)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+        for a, b in evs:
+            with torch.cuda.stream(comm):
+                a.record(comm)
+                g(outs[0][:F])
+                b.record(comm)
+        torch.cuda.synchronize()
+        mine = {"rank": rank, "rows": rows, "render_ms_per_frame": round(kernel_ms / F, 4),
+                "gather_ms_per_launch": round(float(np.mean([a.elapsed_time(b) for a, b in evs])), 4)}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        r_ms = [r["render_ms_per_frame"] for r in allr]
+        ranks_rec = {"per_rank": allr, "render_ms_per_frame_max": max(r_ms), "render_ms_per_frame_min": min(r_ms),
+                     "imbalance": round(max(r_ms) / min(r_ms), 4),
+                     "gather_ms_per_launch_max": max(r["gather_ms_per_launch"] for r in allr),
+                     "what": "untimed: one launch of F frames of each rank's rows (HIP events) and one gather of "
+                             "F frames to rank 0 (HIP events on the gather stream); ms_per_step is the timed run"}
 
     samples = W * H * spp
     value = samples * args.steps / elapsed / 1e6
@@ -397,6 +438,7 @@ def main() -> int:
     if dist_rec:
         rec["rccl_world"] = dist_rec["world"] if backend == "nccl" else None
         rec["dist"] = dist_rec
+        rec["ranks"] = ranks_rec
     if world > 1 and backend != "nccl":
         rec["rehearsal_backend"] = backend  # code-path check only, not a measurement
     if rank == 0:
@@ -485,8 +527,14 @@ def main() -> int:
         if world == 1 and not args.no_e2e:
             rec["e2e"] = e2e_timings(_lib, spheres, bg, cam, W, H, depth, spp, seed)
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed,
-                                               args.cpu_row_step or auto_row_step(len(spheres), W, H, spp))
+            row_step = args.cpu_row_step or auto_row_step(len(spheres), W, H, spp)
+            rec["cpu_baseline"], ref = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed, row_step,
+                                                    args.cpu_min_seconds)
+            rec["parity"] = device_parity(torch, _lib, scene, cam, params, F, launch, outs[0], ref, row_step)
+        else:
+            rec["parity"] = None
+            rec["parity_null_reason"] = ("measured at N = 1 (the oracle frame is cpu_baseline's)" if world > 1
+                                         else "--no-cpu-baseline: no oracle frame")
     if rank == 0:
         print(json.dumps(rec), flush=True)
     for sc in scenes:
@@ -568,22 +616,80 @@ def cpu_share() -> tuple:
     return cores, "min of " + ", ".join(f"{k}={v}" for k, v in seen.items())
 
 
-def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step):
+def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step, min_seconds=0.0):
     """Oracle (C FP64 port of the reference CPU path, chunk-queue scheduler of
-    ray/tracer.go:86-116) on every `row_step`-th row of the same frame."""
+    ray/tracer.go:86-116) on every `row_step`-th row of the same frame, pass 0;
+    while less than `min_seconds` have passed, passes 1, 2, ... of the same rows
+    (a frame as small as C1's renders in well under a second). Returns the
+    record and pass 0's (rows, segments) for the parity check."""
     from oracle import oracle as O
 
     cores, why = cpu_share()
     rows = np.arange(0, H, row_step, dtype=np.int32)
     bg = np.array([1.0, 1.0, 1.0, 0.4, 0.65, 1.0])
     t0 = time.perf_counter()
-    O.render_rows(spheres, bg, camera, W, H, spp, depth, 0.5, seed, rows, workers=cores, segments=False)
+    ref = O.render_rows(spheres, bg, camera, W, H, spp, depth, 0.5, seed, rows, workers=cores, segments=True)
+    passes = 1
+    while time.perf_counter() - t0 < min_seconds:
+        O.render_rows(spheres, bg, camera, W, H, spp, depth, 0.5, seed, rows, workers=cores, segments=False,
+                      pass_=passes)
+        passes += 1
     dt = time.perf_counter() - t0
-    samples = len(rows) * W * spp
-    return {"value": round(samples / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "seconds": round(dt, 3), "cpu_model": cpu_model(), "cores_reason": why,
-            "sample": f"every {row_step}. row of the same frame ({len(rows)} rows x {W} px x r={spp}), "
-                      f"oracle/tray_oracle.c, {cores} pthreads"}
+    samples = len(rows) * W * spp * passes
+    what = f"{len(rows)} rows x {W} px x r={spp}" + (f" x {passes} passes" if passes > 1 else "")
+    return ({"value": round(samples / dt / 1e6, 4), "unit": "Mrays/s", "cores": cores, "kind": "port",
+             "seconds": round(dt, 3), "cpu_model": cpu_model(), "cores_reason": why, "passes": passes,
+             "sample": f"every {row_step}. row of the same frame ({what}), oracle/tray_oracle.c, {cores} pthreads"},
+            (rows, ref))
+
+
+def frame_parity(ref, ref_seg, f64, seg, f32, tol=1e-4):
+    """Per-pixel parity of device frames against the oracle's frame of the same
+    pass (ray/tracer.go:120-155): `f64` (TRAY_OUT_RGB_F64) and `f32`
+    (TRAY_OUT_RGB_F32) are [rows, W, 3], `seg`/`ref_seg` the per-pixel Scene.Hit
+    counts. The f32 bound: one f32 rounding (<= 2^-24 |v|) of a value within
+    1e-12 of the oracle's mean."""
+    ref = np.asarray(ref, dtype=np.float64)
+    d64 = np.abs(np.asarray(f64, dtype=np.float64) - ref)
+    g32 = np.asarray(f32, dtype=np.float32)
+    d32 = np.abs(g32.astype(np.float64) - ref)
+    linf = float(d64.max()) if d64.size else 0.0
+    linf32 = float(d32.max()) if d32.size else 0.0
+    rec = {"pixels": int(ref.shape[0] * ref.shape[1]), "rows": int(ref.shape[0]), "linf": linf, "linf_f32": linf32,
+           "segments_equal": bool(np.array_equal(seg, ref_seg)), "segments_differing": int((seg != ref_seg).sum()),
+           "f64_bit_equal_frac": round(float((f64 == ref).mean()), 4),
+           "f32_within_one_rounding": bool(np.all(d32 <= np.abs(ref) * 2.0**-24 + 1e-12)),
+           "f32_equal_frac": round(float((g32 == ref.astype(np.float32)).mean()), 4),
+           "tol": tol}
+    rec["ok"] = bool(rec["segments_equal"] and linf <= tol and linf32 <= tol and np.isfinite(ref).all())
+    return rec
+
+
+def device_parity(torch, _lib, scene, cam, params, F, launch, out, oracle_frame, row_step):
+    """Untimed: pass 0 of the frame on the device, (a) through tray_render_async into
+    TRAY_OUT_RGB_F64 with segment counts and (b) as frame 0 of a passes launch in
+    the timed shape (slot 0: F frames into TRAY_OUT_RGB_F32), against the oracle's
+    pass 0 that cpu_baseline rendered, on the rows the oracle rendered."""
+    rows_idx, (ref, ref_seg) = oracle_frame
+    W, H = params.width, params.height
+    p = _lib.Params.from_buffer_copy(params)
+    p.output, p.pass_ = _lib.OUT_RGB_F64, 0
+    f64 = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+    seg = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    scene.render_async(cam._state, p, f64.data_ptr(), seg.data_ptr(), stream.cuda_stream)
+    with torch.cuda.stream(stream):
+        launch(0, 0, F)  # frames 0 .. F-1 into `out`, exactly as the timed launches render them
+    torch.cuda.synchronize()
+    idx = torch.as_tensor(rows_idx, dtype=torch.long, device="cuda")
+    rec = frame_parity(ref, ref_seg, f64[idx].cpu().numpy(), seg[idx].cpu().numpy().astype(np.uint32),
+                       out[0][idx].cpu().numpy())
+    rec["pass"] = 0
+    rec["scope"] = ("the whole frame" if row_step == 1 else
+                    f"every {row_step}. row ({len(rows_idx)} of {H} rows: the rows cpu_baseline rendered)")
+    rec["reference"] = "oracle/tray_oracle.c (ray/*.go restated; per-pixel parity with the Go binary's " \
+                       "fortio.org/rand stream is unpinned, DESIGN.md 3)"
+    return rec
 
 
 if __name__ == "__main__":

@@ -267,7 +267,19 @@ int tray_render_devices_progress(const tray_sphere *spheres, int32_t n_spheres, 
                                  void *user);
 
 /* Device-resident scene for repeated renders (the scene is read-only during
- * Render, ray/tracer.go:48). */
+ * Render, ray/tracer.go:48).
+ *
+ * Concurrency: like a Go *Scene, which several goroutines may Render at once, a
+ * scene handle may be used by any number of tray_render_*_async calls, from any
+ * threads and on any streams, without ordering them. Every render takes one of
+ * the scene's launch contexts (its work queue, sample or chunk buffer,
+ * candidate records and traversal-stack overflow area) for as long as it runs:
+ * the one last used on the same stream, else an idle one, else a new one (up to
+ * 4 per scene), else the least recently used, which the new render's stream
+ * then waits for on the device (hipStreamWaitEvent). Buffers grow only after
+ * the renders using them have finished. Results do not depend on which context
+ * a render takes. tray_scene_release waits for the scene's enqueued renders and
+ * must not race with a call still enqueueing on the same handle. */
 int tray_scene_upload(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,
                       int32_t device, tray_scene_t *out);
 int tray_scene_release(tray_scene_t scene);
@@ -311,7 +323,8 @@ int tray_render_plan_get(tray_scene_t scene, const tray_camera *camera, const tr
 
 /* Asynchronous render into DEVICE memory on `stream` (a hipStream_t, or NULL for
  * the null stream of the scene's device). out_device: compact rows in the
- * params->output format; segments_device nullable. Returns after enqueueing. */
+ * params->output format; segments_device nullable. Returns after enqueueing.
+ * Safe beside other renders of the same scene on other streams (see above). */
 int tray_render_async(tray_scene_t scene, const tray_camera *camera, const tray_params *params, void *out_device,
                       uint32_t *segments_device, void *stream);
 

@@ -26,6 +26,9 @@
  *   "wave_chunks"         chunks a wave reserves per work-queue take (1..64), for
  *                         the whole launch (default: the build's size, single
  *                         chunks near the end of the queue) (same bits)
+ *   "scene_contexts"      launch contexts per scene (default 4): renders of one
+ *                         scene beyond this many in flight wait for the least
+ *                         recently used one; 1 serialises them (same bits)
  */
 #ifndef TRAY_DEBUG_H
 #define TRAY_DEBUG_H

@@ -118,3 +118,51 @@ def test_profile_records_only_for_the_loaded_device_code(tmp_path):
     assert got is None and "None" in why  # records from before the hash existed are not trusted
     got, _, why = bench._profile_json("pmc_mix", "c9", 16, h, profiles_dir=str(tmp_path))
     assert got is None and "no pmc_mix_c9.json" in why
+
+
+def test_rank_stuck_in_a_collective_is_stopped_and_named(tmp_path, capsys):
+    """Rank 1 sleeps past the limit while rank 0 waits for it in a gloo barrier (a
+    rank stuck in the gather): the launcher stops both within the limit, exits
+    non-zero and names the ranks it stopped."""
+    import time
+
+    script = _script(tmp_path, "import torch.distributed as dist\n"
+                               "dist.init_process_group('gloo')\n"
+                               "if os.environ['RANK'] == '1': time.sleep(120)\n"
+                               "dist.barrier()\n")
+    t0 = time.monotonic()
+    rc = bench.launch_ranks(2, [], timeout=20.0, script=script)
+    took = time.monotonic() - t0
+    assert rc == 124 and took < 40
+    err = capsys.readouterr().err
+    assert "rank(s) [0, 1] still running after 20.0 s" in err
+
+
+def test_rank_timeout_has_a_finite_default():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0
+    import re
+
+    m = re.search(r"--rank-timeout RANK_TIMEOUT", r.stdout)
+    assert m
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'ap.add_argument("--rank-timeout", type=float, default=900.0' in src
+
+
+def test_frame_parity_record():
+    """bench.frame_parity (the `parity` field of the bench line) on synthetic frames."""
+    import numpy as np
+
+    rng = np.random.default_rng(1)
+    ref = rng.random((4, 5, 3))
+    seg = rng.integers(64, 200, (4, 5)).astype(np.uint32)
+    rec = bench.frame_parity(ref, seg, ref.copy(), seg.copy(), ref.astype(np.float32))
+    assert rec["ok"] and rec["linf"] == 0.0 and rec["pixels"] == 20 and rec["segments_equal"]
+    assert rec["f32_within_one_rounding"] and rec["f32_equal_frac"] == 1.0
+    bad = ref.copy()
+    bad[1, 2, 0] += 2e-4
+    seg2 = seg.copy()
+    seg2[0, 0] += 1
+    rec = bench.frame_parity(ref, seg, bad, seg2, ref.astype(np.float32))
+    assert not rec["ok"] and abs(rec["linf"] - 2e-4) < 1e-12 and rec["segments_differing"] == 1

@@ -614,3 +614,38 @@ def test_wave_chunk_reservations_are_invisible(L, O, knobs, chunks):
         assert np.array_equal(base[(str({}), None)][1], one)  # frame k of the launch = pass 1 + k rendered alone
     finally:
         dev.release()
+
+
+def test_config2_full_frame_vs_oracle(L, O):
+    """The headline config (C2: 1280x720, r=64, d=50, seed 2) at EVERY one of its
+    921,600 pixels against the oracle's render of the same pass (ray/tracer.go:
+    120-155 restated): per-pixel Scene.Hit counts bit-exact, the FP64 output
+    (tray_render, fixed-point pixel sums) within 1e-12, and frame 0 of a
+    16-pass launch in bench.py's timed shape (TRAY_OUT_RGB_F32) within one f32
+    rounding of a value inside 1e-12 (bench.frame_parity, the `parity` field of
+    the bench line)."""
+    import torch
+
+    from bench import frame_parity
+
+    W, H, spp, depth, seed = 1280, 720, 64, 50, 2
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, W, H)
+    f64, seg = gpu_render(L, sc, DEFAULT_BG, st, W, H, spp, depth, 0.5, seed)
+    dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
+    try:
+        out = torch.empty((16, H, W, 3), dtype=torch.float32, device="cuda")
+        p = L.make_params(W, H, depth, spp, 0.5, seed, output=L.OUT_RGB_F32)
+        assert dev.plan(st, p, 16).acc_slots > 0  # the on-chip sums bench.py times
+        dev.render_passes_async(st, p, 16, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        f32 = out[0].cpu().numpy()
+    finally:
+        dev.release()
+    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), W, H, spp, depth, 0.5, seed, workers=WORKERS)
+    rec = frame_parity(ref, rseg, f64, seg, f32)
+    assert rec["pixels"] == W * H
+    assert rec["segments_equal"], rec
+    assert rec["linf"] <= TOL and rec["linf"] <= TIGHT, rec
+    assert rec["f32_within_one_rounding"] and rec["linf_f32"] <= TOL, rec
+    assert rec["ok"]

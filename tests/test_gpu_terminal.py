@@ -55,9 +55,11 @@ def test_rendered_frame_to_terminal(L, O):
 
 
 def test_scale_async_stays_in_stream_order(L, O):
-    """tray_scale_rgba_async only enqueues: it returns while a C2-sized render
-    queued before it on the same stream is still running (no host sync, no copy
-    outside the stream), and the scaled bytes are those of the finished frame."""
+    """tray_scale_rgba_async only enqueues: it returns while the work queued
+    before it on the same stream has not started (no host sync, no copy outside
+    the stream), and the scaled bytes are those of the finished frame. The
+    stream is held by a spin kernel of >= 0.1 s ahead of the render, so the check
+    does not race the render's ~5 ms."""
     import torch
 
     from tray_amd import ray
@@ -71,7 +73,9 @@ def test_scale_async_stays_in_stream_order(L, O):
         frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
         dst = torch.zeros((24, 40, 4), dtype=torch.uint8, device="cuda")
         p = L.make_params(W, H, 50, 64, 0.5, 2, output=L.OUT_RGBA8)
-        dev.render_async(cam._state, p, frame.data_ptr(), None, stream.cuda_stream)  # ~5 ms of work
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(300_000_000)  # 0.12 s at the shader clock (3 s if it counts the 100-MHz one)
+        dev.render_async(cam._state, p, frame.data_ptr(), None, stream.cuda_stream)
         L.check(L.lib().tray_scale_rgba_async(frame.data_ptr(), W, H, dst.data_ptr(), 40, 24, L.SCALE_BILINEAR, 0,
                                               stream.cuda_stream))
         still_running = not stream.query()
@@ -90,3 +94,39 @@ def test_scale_after_shutdown(L, O):
     assert np.array_equal(L.scale_rgba(img, 30, 17, bilinear=True), ref)
     L.check(L.lib().tray_shutdown())
     assert np.array_equal(L.scale_rgba(img, 30, 17, bilinear=True), ref)
+
+
+def test_scale_beside_shutdown_threads(L, O):
+    """tray_shutdown frees idle staging buffers while another thread scales:
+    entries keep their addresses (a list), so a scale holding one outside the
+    lock never sees it moved or freed. Every scaled image is right."""
+    import threading
+
+    img = rgba(45, 80, seed=13, opaque=False)
+    ref = O.scale_rgba(img, 30, 17, bilinear=True)
+    stop = threading.Event()
+    bad, errors = [], []
+
+    def scaler():
+        try:
+            for _ in range(60):
+                if not np.array_equal(L.scale_rgba(img, 30, 17, bilinear=True), ref):
+                    bad.append(1)
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+        finally:
+            stop.set()
+
+    def closer():
+        try:
+            while not stop.is_set():
+                L.check(L.lib().tray_shutdown())
+        except BaseException as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=scaler), threading.Thread(target=scaler), threading.Thread(target=closer)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not errors and not bad

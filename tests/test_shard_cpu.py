@@ -145,3 +145,41 @@ def test_frame_gather_equals_round3_gather(tmp_path, world):
     path = str(tmp_path / "ok.npy")
     mp.spawn(_worker_framegather, args=(world, _free_port(), path), nprocs=world, join=True)
     assert np.load(path).all()
+
+
+def _worker_owned(rank, world, port, result_path):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tray_amd import shard
+
+    ok = True
+    kept = []
+    for call in range(shard._GATHERS_MAX + 3):  # more shapes than the cache keeps, then the first again
+        height = 9 + (call % (shard._GATHERS_MAX + 2))
+        rows = shard.rows_for(height, 1, world, rank)
+        frame = torch.full((2, height, 5, 3), float(call))
+        got = shard.gather_frames(frame[:, torch.as_tensor(rows, dtype=torch.long)].contiguous(), height, 1, world,
+                                  rank)
+        if rank == 0:
+            kept.append((got, frame))
+            ok &= all(bool(torch.equal(g, f)) for g, f in kept)  # earlier results untouched by later gathers
+        else:
+            ok &= got is None
+        ok &= len(shard._GATHERS) <= shard._GATHERS_MAX
+    flags = [None] * world
+    dist.all_gather_object(flags, ok)
+    if rank == 0:
+        np.save(result_path, np.array(flags))
+    dist.destroy_process_group()
+
+
+def test_gather_frames_returns_owned_tensors(tmp_path):
+    """gather_frames / gather_image return tensors of the caller's own: a later
+    gather of the same shape does not overwrite an earlier result, and the
+    per-shape buffers kept between calls are bounded."""
+    path = str(tmp_path / "ok.npy")
+    mp.spawn(_worker_owned, args=(2, _free_port(), path), nprocs=2, join=True)
+    assert np.load(path).all()

@@ -160,7 +160,7 @@ EXPORTS = (
 # include/tray_debug.h: test / A-B hooks outside the stable ABI (not in EXPORTS).
 DEBUG_EXPORTS = ("tray_debug_set", "tray_debug_clear")
 DEBUG_KNOBS = ("acc_slots", "band_samples", "bvh_leaf", "bvh_lds_mode", "stack_lds_slots", "node_deep",
-               "primary_candidates", "resolve_staged", "wave_chunks")
+               "primary_candidates", "resolve_staged", "wave_chunks", "scene_contexts")
 
 # tray_progress_fn: void (*)(int32_t rows, void *user)
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_void_p)
@@ -445,9 +445,9 @@ def linear_to_srgba_async(rgb_ptr: int, n_pixels: int, rgba_ptr: int, device: in
 
 
 class DeviceScene:
-    """A scene uploaded once to one device (tray_scene_upload); render many times.
-    Renders of one DeviceScene must be ordered on one stream (shared work queue and
-    sample buffer)."""
+    """A scene uploaded once to one device (tray_scene_upload); render many times,
+    from any thread and on any streams: each render runs in a launch context of
+    its own (work queue, sample buffer, candidate records; include/tray.h)."""
 
     def __init__(self, spheres, background: Background, device: int = 0, lib_path: str | None = None):
         self.L = lib(lib_path)

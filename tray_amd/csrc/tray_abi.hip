@@ -39,7 +39,7 @@ static std::atomic<long long> g_knob_value[kKnobCount];
 static std::atomic<bool> g_knob_set[kKnobCount];
 static const char* const kKnobNames[kKnobCount] = {
     "acc_slots", "band_samples", "bvh_leaf", "bvh_lds_mode", "stack_lds_slots", "node_deep", "primary_candidates",
-    "resolve_staged", "wave_chunks"};
+    "resolve_staged", "wave_chunks", "scene_contexts"};
 
 bool debug_knob(DebugKnob k, long long* v) {
     if (!g_knob_set[k].load(std::memory_order_acquire)) return false;
@@ -169,9 +169,6 @@ int device_usable(int32_t device) {
 
 }  // namespace tray
 
-// A scene resident on one device. Renders of one scene handle share its work
-// queue counter, so they must be ordered on one stream (the queue is zero when
-// a launch starts: zeroed at allocation, then by each band's resolve pass).
 // What a primary-ray candidate list depends on (compared byte for byte).
 struct CandKey {
     tray_camera cam;
@@ -179,13 +176,44 @@ struct CandKey {
     int32_t width, height, y_start, rows, tile_rows, tile_count, tile_index, multi_sample;
 };
 
+// The mutable device state ONE render uses while it runs: the work-queue word
+// (zero between launches: zeroed at allocation, then by each band's resolve
+// pass), the per-sample buffer or chunk records of a launch band, the primary-ray
+// candidate records of the last camera and row set it rendered, and the
+// traversal-stack overflow area (deep BVHs). `done` is recorded on the render's
+// stream after each launch that used it. A scene holds a few of these, so that
+// renders of one scene on different streams (or threads) run concurrently
+// without sharing any of it, as several goroutines may Render one read-only
+// *Scene at once (ray/tracer.go:48, ray/objects.go:37-46).
+struct LaunchCtx {
+    uint32_t* queue = nullptr;
+    double* samples = nullptr;
+    size_t samples_bytes = 0;
+    uint4* cand = nullptr;
+    size_t cand_bytes = 0;
+    bool cand_valid = false;
+    CandKey cand_key;
+    uint32_t* stack_ovf = nullptr;
+    size_t ovf_bytes = 0;
+    hipEvent_t done = nullptr;
+    bool launched = false;          // `done` has been recorded
+    hipStream_t last_stream = nullptr;
+    uint64_t last_use = 0;          // the scene's launch count at its last launch
+};
+
+// Launch contexts per scene: renders beyond this many in flight at once wait
+// (on the device, hipStreamWaitEvent) for the least recently used one.
+constexpr int kSceneContexts = 4;
+
+// A scene resident on one device. Its arrays are read-only after the upload;
+// everything a render writes lives in a launch context (above), taken under the
+// scene's mutex for the time it takes to enqueue the render.
 struct tray_scene_s {
     int32_t device;
     int32_t n;
     int32_t n_pad;
     double4* geo;  // n_pad entries, NaN-padded (see tray::KernelParams::geo)
     tray::MatRec* mat;
-    uint32_t* queue;
     tray::V3 bg_a, bg_b;
     double max_att;  // max(1, |albedo| of every Lambertian/Metal sphere): bounds a path's throughput
     // exact-culling BVH (absent for tiny or non-finite scenes)
@@ -194,24 +222,17 @@ struct tray_scene_s {
     int32_t n_nodes, n_slots, n_leaves, stack_cap, leaf_max, n_global;
     tray::Bvh4Node* nodes;
     int32_t* leaves;
-    uint32_t* stack_ovf;  // traversal-stack slots beyond LDS (deep BVHs only)
+    size_t ovf_bytes;  // traversal-stack overflow area a render needs (deep BVHs only; per context)
     double4* bgeo;
     int32_t* bidx;
     tray::MatRec* bmat;
-    // One device allocation holds geo, mat, queue, srgb and the BVH arrays (the
-    // pointers above point into it); stack_ovf, samples and cand are separate.
+    // One device allocation holds geo, mat, srgb and the BVH arrays (the pointers
+    // above point into it).
     void* arena;
-    // Per-sample path colours of one launch band (tray_kernel.hpp), grown on
-    // demand: renders of one scene must be ordered (one stream, or synchronised).
-    double* samples;
-    size_t samples_bytes;
     double* srgb;  // the RGBA8 encoder table (tray::srgb_thresholds), 256 doubles
-    // Primary-ray candidates of the last camera and row set rendered (BVH scenes;
-    // launch_cand_build), rebuilt on the render stream when either changes.
-    uint4* cand;
-    size_t cand_bytes;
-    bool cand_valid;
-    CandKey cand_key;
+    std::mutex mu;  // guards ctx and launches
+    std::vector<LaunchCtx*> ctx;
+    uint64_t launches;
 };
 
 using namespace tray;
@@ -379,7 +400,8 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->n_slots = (int32_t)bvh.geo.size();
     sc->n_leaves = (int32_t)bvh.leaves.size();
     sc->leaves = nullptr;
-    sc->stack_ovf = nullptr;
+    sc->ovf_bytes = 0;
+    sc->launches = 0;
     sc->stack_cap = bvh.stack_max + kStackSlack;
     sc->leaf_max = has_bvh ? bvh.leaf_max : 0;
     sc->n_global = has_bvh ? bvh.n_global : 0;
@@ -387,12 +409,7 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->bgeo = nullptr;
     sc->bidx = nullptr;
     sc->bmat = nullptr;
-    sc->samples = nullptr;
-    sc->samples_bytes = 0;
     sc->srgb = nullptr;
-    sc->cand = nullptr;
-    sc->cand_bytes = 0;
-    sc->cand_valid = false;
     std::vector<MatRec> bmat(bvh.idx.size());
     for (size_t i = 0; i < bvh.idx.size(); ++i) {
         const int32_t k = bvh.idx[i];
@@ -403,7 +420,6 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     sc->n_pad = n_pad;
     sc->geo = nullptr;
     sc->mat = nullptr;
-    sc->queue = nullptr;
     sc->max_att = 1.0;
     for (int32_t i = 0; i < n; ++i)
         if (spheres[i].material != TRAY_DIELECTRIC)  // Dielectric attenuates by exactly 1
@@ -423,7 +439,6 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
     };
     const Part parts[] = {
         {(void**)&sc->geo, geo.data(), sizeof(double4) * (size_t)n_pad},
-        {(void**)&sc->queue, nullptr, sizeof(uint32_t)},
         {(void**)&sc->srgb, srgb_thresholds(), 256 * sizeof(double)},
         {(void**)&sc->mat, mat.data(), sizeof(MatRec) * (size_t)n},
         {(void**)&sc->nodes, bvh.nodes.data(), has_bvh ? sizeof(Bvh4Node) * bvh.nodes.size() : 0},
@@ -450,13 +465,9 @@ int tray_scene_upload(const tray_sphere* spheres, int32_t n, const tray_backgrou
         for (size_t i = 0; i < sizeof(parts) / sizeof(parts[0]); ++i)  // empty arrays stay null
             *parts[i].dst = parts[i].bytes ? static_cast<uint8_t*>(sc->arena) + offsets[i] : nullptr;
     }
-    if (e == hipSuccess && has_bvh) {
-        const size_t ovf = bvh_stack_overflow_bytes(bvh.stack_max + kStackSlack, device);
-        if (ovf) e = hipMalloc(&sc->stack_ovf, ovf);
-    }
+    if (has_bvh) sc->ovf_bytes = bvh_stack_overflow_bytes(bvh.stack_max + kStackSlack, device);
     if (e != hipSuccess) {
         (void)hipFree(sc->arena);
-        (void)hipFree(sc->stack_ovf);
         delete sc;
         return hip_fail(e, "scene upload");
     }
@@ -479,13 +490,25 @@ int tray_scene_get_info(tray_scene_t sc, tray_scene_info* out) {
     return TRAY_OK;
 }
 
+static void free_ctx(LaunchCtx* c) {
+    if (c->launched) (void)hipEventSynchronize(c->done);  // its last render, on whatever stream
+    if (c->queue) (void)hipFree(c->queue);
+    if (c->samples) (void)hipFree(c->samples);
+    if (c->cand) (void)hipFree(c->cand);
+    if (c->stack_ovf) (void)hipFree(c->stack_ovf);
+    if (c->done) (void)hipEventDestroy(c->done);
+    delete c;
+}
+
 int tray_scene_release(tray_scene_t sc) {
     if (!sc) return TRAY_OK;
     (void)hipSetDevice(sc->device);
+    {
+        std::lock_guard<std::mutex> lk(sc->mu);
+        for (LaunchCtx* c : sc->ctx) free_ctx(c);  // waits for the renders still enqueued
+        sc->ctx.clear();
+    }
     if (sc->arena) (void)hipFree(sc->arena);
-    if (sc->stack_ovf) (void)hipFree(sc->stack_ovf);
-    if (sc->samples) (void)hipFree(sc->samples);
-    if (sc->cand) (void)hipFree(sc->cand);
     delete sc;
     return TRAY_OK;
 }
@@ -544,7 +567,6 @@ static int prepare_render(tray_scene_t sc, const tray_camera* cam, const tray_pa
     k.mat = sc->mat;
     k.n = sc->n;
     k.n_pad = sc->n_pad;
-    k.queue = sc->queue;
     k.width = p->width;
     k.height = p->height;
     k.spp = p->rays_per_pixel;
@@ -589,7 +611,6 @@ static int prepare_render(tray_scene_t sc, const tray_camera* cam, const tray_pa
     k.n_global = sc->n_global;
     k.leaves = sc->leaves;
     k.leaf_single = sc->leaf_max == 1 ? 1 : 0;
-    k.stack_ovf = sc->stack_ovf;
     k.stack_cap = sc->stack_cap;
     // The BVH's conservative FP32 box test assumes every ray origin lies within
     // [-M, M]^3 (tray_bvh.cpp): hit points do; check the camera and lens disc.
@@ -601,8 +622,63 @@ static int prepare_render(tray_scene_t sc, const tray_camera* cam, const tray_pa
     return TRAY_OK;
 }
 
+// The scene's launch context for a render on `stream` (called with sc->mu held):
+// the one last used on this stream (stream order already serialises it), else
+// an idle one (never launched, or its last render has finished), else a new one
+// while the scene has fewer than kSceneContexts, else the least recently used,
+// which the stream then waits for on the device. Either way the stream is made
+// to wait for the context's last render, so nothing it enqueues can overlap it.
+static int take_ctx(tray_scene_t sc, hipStream_t stream, LaunchCtx** out) {
+    long long cap = kSceneContexts;
+    if (debug_knob(kKnobSceneContexts, &cap)) cap = std::max(1LL, std::min(cap, 64LL));
+    LaunchCtx* pick = nullptr;
+    for (LaunchCtx* c : sc->ctx)
+        if (c->launched && c->last_stream == stream && (!pick || c->last_use > pick->last_use)) pick = c;
+    if (!pick)
+        for (LaunchCtx* c : sc->ctx)
+            if ((!c->launched || hipEventQuery(c->done) == hipSuccess) && (!pick || c->last_use > pick->last_use))
+                pick = c;
+    if (!pick && (long long)sc->ctx.size() < cap) {
+        LaunchCtx* c = new LaunchCtx();
+        hipError_t e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->queue), 256);
+        if (e == hipSuccess) e = hipMemset(c->queue, 0, sizeof(uint32_t));
+        if (e != hipSuccess) {
+            free_ctx(c);
+            return hip_fail(e, "launch context");
+        }
+        sc->ctx.push_back(c);
+        pick = c;
+    }
+    if (!pick)
+        for (LaunchCtx* c : sc->ctx)
+            if (!pick || c->last_use < pick->last_use) pick = c;
+    if (pick->launched && hipEventQuery(pick->done) != hipSuccess)
+        TRAY_HIP(hipStreamWaitEvent(stream, pick->done, 0));
+    *out = pick;
+    return TRAY_OK;
+}
+
+// Grows a context buffer to `bytes` (contents not kept). The context's last
+// render may still run on another stream: wait for it before freeing.
+static hipError_t grow_ctx_buffer(LaunchCtx* c, void** buf, size_t* have, size_t bytes) {
+    if (*have >= bytes) return hipSuccess;
+    if (*buf) {
+        if (c->launched) {
+            const hipError_t e = hipEventSynchronize(c->done);
+            if (e != hipSuccess) return e;
+        }
+        (void)hipFree(*buf);
+        *buf = nullptr;
+        *have = 0;
+    }
+    const hipError_t e = hipMalloc(buf, bytes);
+    if (e == hipSuccess) *have = bytes;
+    return e;
+}
+
 static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray_params* p, void* out_device,
-                             uint32_t* segments_device, unsigned long long* stats_device, void* stream,
+                             uint32_t* segments_device, unsigned long long* stats_device, void* stream_arg,
                              int32_t n_passes = 1, unsigned long long* progress_device = nullptr) {
     if (!out_device) return fail(TRAY_ERR_INVALID_ARGUMENT, "null argument");
     KernelParams k;
@@ -613,20 +689,19 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.segments = segments_device;
     k.stats = stats_device;
     k.progress = progress_device;
+    const hipStream_t stream = static_cast<hipStream_t>(stream_arg);
     TRAY_HIP(hipSetDevice(sc->device));
-    const uint64_t spp_launch = (uint64_t)p->rays_per_pixel * (uint64_t)n_passes;
-    const size_t need = accum_buffer_bytes(p->width, k.rows, spp_launch, launch_layout(k, use_bvh).acc_slots > 0);
-    if (need > sc->samples_bytes) {
-        if (sc->samples) {
-            TRAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-            TRAY_HIP(hipFree(sc->samples));
-            sc->samples = nullptr;
-            sc->samples_bytes = 0;
-        }
-        TRAY_HIP(hipMalloc(&sc->samples, need));
-        sc->samples_bytes = need;
-    }
-    k.samples = sc->samples;
+    const LaunchPlan plan = plan_launch(k, use_bvh);  // decided once: the buffer and the bands agree
+    std::lock_guard<std::mutex> lk(sc->mu);
+    LaunchCtx* c = nullptr;
+    rc = take_ctx(sc, stream, &c);
+    if (rc) return rc;
+    TRAY_HIP(grow_ctx_buffer(c, reinterpret_cast<void**>(&c->samples), &c->samples_bytes, plan.buffer_bytes));
+    if (use_bvh && k.stack_cap > plan.layout.stack_lds)
+        TRAY_HIP(grow_ctx_buffer(c, reinterpret_cast<void**>(&c->stack_ovf), &c->ovf_bytes, sc->ovf_bytes));
+    k.queue = c->queue;
+    k.samples = c->samples;
+    k.stack_ovf = c->stack_ovf;
     if (use_bvh && cand_enabled() && sc->n_slots - sc->n_global <= kCandMaxSpheres) {
         CandKey key;
         memset(&key, 0, sizeof(key));
@@ -635,27 +710,27 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         key.width = p->width, key.height = p->height, key.y_start = p->y_start, key.rows = k.rows;
         key.tile_rows = k.tile_rows, key.tile_count = k.tile_count, key.tile_index = k.tile_index;
         key.multi_sample = p->rays_per_pixel > 1;
-        if (!sc->cand_valid || memcmp(&key, &sc->cand_key, sizeof(key)) != 0) {
-            const size_t bytes = cand_workspace_bytes(p->width, k.rows);
-            if (bytes > sc->cand_bytes) {
-                if (sc->cand) {
-                    TRAY_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-                    TRAY_HIP(hipFree(sc->cand));
-                    sc->cand = nullptr;
-                    sc->cand_bytes = 0;
-                }
-                sc->cand_valid = false;
-                TRAY_HIP(hipMalloc(&sc->cand, bytes));
-                sc->cand_bytes = bytes;
-            }
-            sc->cand_valid = false;
-            TRAY_HIP(launch_cand_build(k, sc->cand, static_cast<hipStream_t>(stream)));
-            sc->cand_key = key;
-            sc->cand_valid = true;
+        if (!c->cand_valid || memcmp(&key, &c->cand_key, sizeof(key)) != 0) {
+            c->cand_valid = false;
+            TRAY_HIP(grow_ctx_buffer(c, reinterpret_cast<void**>(&c->cand), &c->cand_bytes,
+                                     cand_workspace_bytes(p->width, k.rows)));
+            TRAY_HIP(launch_cand_build(k, c->cand, stream));
+            c->cand_key = key;
+            c->cand_valid = true;
         }
-        k.cand = sc->cand;
+        k.cand = c->cand;
     }
-    TRAY_HIP(launch_render(k, use_bvh, static_cast<hipStream_t>(stream), sc->samples_bytes));
+    const hipError_t e = launch_render(k, use_bvh, plan, stream, c->samples_bytes);
+    // Recorded even after a failure: a band may already be enqueued.
+    const hipError_t r = hipEventRecord(c->done, stream);
+    c->launched = c->launched || r == hipSuccess;
+    c->last_stream = stream;
+    c->last_use = ++sc->launches;
+    if (e != hipSuccess) return hip_fail(e, "launch_render");
+    if (r != hipSuccess) {  // nothing marks the render's end: wait for it here
+        (void)hipStreamSynchronize(stream);
+        return hip_fail(r, "hipEventRecord");
+    }
     return TRAY_OK;
 }
 
@@ -667,15 +742,15 @@ int tray_render_plan_get(tray_scene_t sc, const tray_camera* cam, const tray_par
     bool use_bvh = false;
     int rc = prepare_render(sc, cam, p, n_passes, k, use_bvh);
     if (rc) return rc;
-    const LaunchLayout L = launch_layout(k, use_bvh);
+    const LaunchPlan plan = plan_launch(k, use_bvh);
+    const LaunchLayout& L = plan.layout;
     out->fixed_point_shift = k.acc_shift;
     out->acc_slots = L.acc_slots;
     out->bvh = use_bvh ? 1 : 0;
     out->lds_layout = L.lds_mode;
     out->stack_lds = use_bvh ? L.stack_lds : 0;
     out->lds_bytes = (int64_t)L.lds;
-    out->buffer_bytes = (int64_t)accum_buffer_bytes(p->width, k.rows, (uint64_t)p->rays_per_pixel * (uint64_t)n_passes,
-                                                    L.acc_slots > 0);
+    out->buffer_bytes = (int64_t)plan.buffer_bytes;
     return TRAY_OK;
 }
 
@@ -730,15 +805,19 @@ static int cached_scene(Slot& sl, const tray_sphere* spheres, int32_t n, const t
             return rc;
         }
         if (old) {
-            // The slot's renders are synchronous, so the old scene's sample and
-            // candidate buffers are idle: the new scene takes them over instead of
-            // allocating its own (a C2 frame's 1.4-GB sample buffer: 0.28 ms of
-            // hipFree + hipMalloc per new scene, profiles/r2g_e2e_breakdown.jsonl).
-            std::swap(sc->samples, old->samples);
-            std::swap(sc->samples_bytes, old->samples_bytes);
-            std::swap(sc->cand, old->cand);
-            std::swap(sc->cand_bytes, old->cand_bytes);
-            sc->cand_valid = false;
+            // The slot's renders are synchronous, so the old scene's launch
+            // contexts are idle: the new scene takes them over (their sample and
+            // candidate buffers) instead of allocating its own (a C2 frame's 1.4-GB
+            // sample buffer: 0.28 ms of hipFree + hipMalloc per new scene,
+            // profiles/r2g_e2e_breakdown.jsonl). Their candidate lists were the
+            // old scene's.
+            {
+                std::lock_guard<std::mutex> la(old->mu);
+                std::lock_guard<std::mutex> lb(sc->mu);
+                std::swap(sc->ctx, old->ctx);
+                std::swap(sc->launches, old->launches);
+                for (LaunchCtx* c : sc->ctx) c->cand_valid = false;
+            }
             tray_scene_release(old);
         }
         sl.cached = sc;

@@ -33,6 +33,7 @@ enum DebugKnob {
     kKnobPrimaryCandidates,
     kKnobResolveStaged,
     kKnobWaveChunks,
+    kKnobSceneContexts,
     kKnobCount
 };
 // True, with the value in *v, when the knob is set.

@@ -2153,7 +2153,18 @@ bool band_fits(int32_t width, uint64_t spp) {
     return (uint64_t)((width + 7) / 8) * 64u * spp <= 0x7FFFFFFFull;
 }
 
-hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream, size_t samples_bytes) {
+LaunchPlan plan_launch(const KernelParams& p, bool use_bvh) {
+    LaunchPlan L;
+    L.layout = launch_layout(p, use_bvh);
+    const uint64_t spp_launch = (uint64_t)p.spp * std::max<uint32_t>(p.passes, 1u);
+    const bool partials = L.layout.acc_slots > 0;
+    L.band_tiles = band_tile_rows(p.width, spp_launch, partials);
+    L.buffer_bytes = band_buffer_bytes(p.width, p.rows, spp_launch, partials, L.band_tiles);
+    return L;
+}
+
+hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, hipStream_t stream,
+                         size_t samples_bytes) {
     if (p.rows <= 0) return hipSuccess;
     if (p.passes < 1) p.passes = 1;
     const uint64_t spp_launch = (uint64_t)p.spp * p.passes;
@@ -2167,19 +2178,16 @@ hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream, size_
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (p.acc_shift > 0 && p.spp % 64 != 0) return hipErrorInvalidValue;  // the caller decides (fixed_point_shift)
-    const LaunchLayout layout = launch_layout(p, use_bvh);
+    const LaunchLayout& layout = plan.layout;
     const int lds_mode = layout.lds_mode;
     const size_t lds = layout.lds;
     p.stack_lds = layout.stack_lds;
     p.acc_slots = layout.acc_slots;
     p.acc_off = layout.acc_off;
     if (use_bvh && p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
-    // The caller sized p.samples for this layout and band limit; both read debug knobs
-    // (tray_debug.h), so a knob changed in between must not let a band overrun it: the
-    // band is read once here and checked against the buffer.
-    const int32_t band_tiles = band_tile_rows(p.width, spp_launch, p.acc_slots > 0);
-    if (band_buffer_bytes(p.width, p.rows, spp_launch, p.acc_slots > 0, band_tiles) > samples_bytes)
-        return hipErrorInvalidValue;
+    // The caller sized p.samples from this plan (an invariant: the plan is decided once).
+    const int32_t band_tiles = plan.band_tiles;
+    if (plan.buffer_bytes > samples_bytes) return hipErrorInvalidValue;
     const int threads = use_bvh ? kBvhBlock : 256;
     const bool stats = p.stats != nullptr;
     bool deep = use_bvh && p.n_nodes > kDeepNodes;

@@ -134,9 +134,13 @@ struct KernelParams {
     const uint4* cand;   // nullable (BVH only): primary-ray candidate record per compact pixel (launch_cand_build)
 };
 
-// `samples_bytes`: the capacity of p.samples; a launch whose bands need more is refused
-// (hipErrorInvalidValue) before anything is enqueued.
-hipError_t launch_render(KernelParams p, bool use_bvh, hipStream_t stream, size_t samples_bytes);
+struct LaunchPlan;
+// Enqueues the render of `plan` (plan_launch of the same p and use_bvh): the
+// megakernel and resolve pass of every band. `samples_bytes` is the capacity
+// of p.samples, sized from plan.buffer_bytes by the caller (an internal
+// invariant, checked: hipErrorInvalidValue before anything is enqueued).
+hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, hipStream_t stream,
+                         size_t samples_bytes);
 
 // Fixed-point accumulation. A sample's colour c (already scaled by 2^k through
 // the background) is rounded to the integer v = rint(c), |v| <= 2^kAccBits; any
@@ -177,6 +181,15 @@ struct LaunchLayout {
 LaunchLayout launch_layout(const KernelParams& p, bool use_bvh);
 // Device bytes of the per-sample buffer or (acc_slots > 0) the chunk partials.
 size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials);
+// Everything a launch decides from p and the debug knobs, decided ONCE
+// (plan_launch) and handed to launch_render, so the buffer the caller sizes
+// from it and the bands the launch runs cannot disagree.
+struct LaunchPlan {
+    LaunchLayout layout;
+    int32_t band_tiles;   // 8-row tile rows per launch band
+    size_t buffer_bytes;  // per-sample buffer or chunk records of one band
+};
+LaunchPlan plan_launch(const KernelParams& p, bool use_bvh);
 
 // Primary-ray candidates: for every compact pixel of p's rows, the
 // tree spheres (leaf slots) that any camera ray of the pixel can reach, by a

@@ -27,7 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
-#include <deque>
+#include <list>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -164,7 +164,10 @@ struct Staging {
     bool busy = false;
 };
 static std::mutex g_staging_mu;
-static std::deque<Staging> g_staging;
+// A list: entries keep their addresses while others are added or erased
+// (scale_release_staging may erase idle entries while another thread holds a
+// taken one outside the lock).
+static std::list<Staging> g_staging;
 
 // A buffer of >= bytes on the current device whose last copy has completed.
 static hipError_t staging_take(size_t bytes, Staging** out) {
@@ -182,11 +185,13 @@ static hipError_t staging_take(size_t bytes, Staging** out) {
         if (!pick) pick = &s;  // idle but too small: grow it
     }
     if (!pick) {
+        hipEvent_t done = nullptr;
+        e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+        if (e != hipSuccess) return e;  // nothing added: no entry without an event
         g_staging.emplace_back();
         pick = &g_staging.back();
         pick->device = dev;
-        e = hipEventCreateWithFlags(&pick->done, hipEventDisableTiming);
-        if (e != hipSuccess) return e;
+        pick->done = done;
     }
     if (pick->bytes < bytes) {
         if (pick->host) (void)hipHostFree(pick->host);
@@ -257,8 +262,11 @@ static int scale_enqueue(const uint8_t* src, int32_t sw, int32_t sh, uint8_t* ds
     if (e == hipSuccess) {
         memcpy(stg->host, head.data(), head.size());
         e = hipMemcpyAsync(ws, stg->host, head.size(), hipMemcpyHostToDevice, stream);
-        const hipError_t r = hipEventRecord(stg->done, stream);
-        if (e == hipSuccess) e = r;
+        if (e == hipSuccess) {
+            e = hipEventRecord(stg->done, stream);
+            // No event covers the copy: let it finish before the buffer can be taken again.
+            if (e != hipSuccess) (void)hipStreamSynchronize(stream);
+        }
         staging_give(stg);
     }
     const ScaleSource* d_hs = reinterpret_cast<const ScaleSource*>(ws);

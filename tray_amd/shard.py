@@ -47,19 +47,24 @@ def gather_frames(local, height: int, tile_rows: int, world: int, rank: int, dst
     """gather_image for a batch of frames (the passes of one
     tray_render_passes_async launch): local [n, rows_r, W, C] -> [n, height, W, C]
     on `dst`, with ONE gather for the whole batch (fewer, larger transfers over
-    xGMI). The buffers are allocated once per shape (FrameGather) and the
-    returned frame is a view into one of them: it is valid until the next
-    gather of the same shape. Callers that keep several batches in flight
-    (bench.py's frame slots) hold one FrameGather each."""
+    xGMI). Returns a tensor of the caller's own: the receive buffers are kept
+    per shape (a FrameGather, at most _GATHERS_MAX shapes) and the result is
+    copied out of them. Callers that gather every launch (bench.py's frame
+    slots) hold a FrameGather each and use its zero-copy view instead."""
     key = (tuple(local.shape), str(local.dtype), str(local.device), height, tile_rows, world, rank, dst, id(group))
-    g = _GATHERS.get(key)
+    g = _GATHERS.pop(key, None)
     if g is None:
-        g = _GATHERS[key] = FrameGather(local.shape[0], height, local.shape[2], tuple(local.shape[3:]), tile_rows,
-                                        world, rank, local.dtype, local.device, dst, group)
-    return g(local)
+        g = FrameGather(local.shape[0], height, local.shape[2], tuple(local.shape[3:]), tile_rows, world, rank,
+                        local.dtype, local.device, dst, group)
+    _GATHERS[key] = g  # most recently used last
+    while len(_GATHERS) > _GATHERS_MAX:
+        _GATHERS.pop(next(iter(_GATHERS)))
+    full = g(local)
+    return None if full is None else full.clone()
 
 
 _GATHERS: dict = {}
+_GATHERS_MAX = 4
 
 
 class FrameGather:
