@@ -59,8 +59,9 @@
 extern "C" {
 #endif
 
-#define TRAY_ABI_VERSION 4 /* 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get;
-                              4: TRAY_FLAG_ORDERED_SUM (the library no longer reads the process environment) */
+#define TRAY_ABI_VERSION 5 /* 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get;
+                              4: TRAY_FLAG_ORDERED_SUM (the library no longer reads the process environment);
+                              5: a scene handle may be rendered on several streams at once (launch contexts) */
 
 typedef enum tray_status {
     TRAY_OK = 0,

@@ -642,7 +642,14 @@ static int take_ctx(tray_scene_t sc, hipStream_t stream, LaunchCtx** out) {
         LaunchCtx* c = new LaunchCtx();
         hipError_t e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->queue), 256);
-        if (e == hipSuccess) e = hipMemset(c->queue, 0, sizeof(uint32_t));
+        // Zeroed in the render's stream order: a hipMemset on the null stream is not
+        // ordered before a launch on a non-blocking stream.
+        if (e == hipSuccess) e = hipMemsetAsync(c->queue, 0, sizeof(uint32_t), stream);
+        if (e == hipSuccess) e = hipEventRecord(c->done, stream);  // a later user waits for the zeroing
+        if (e == hipSuccess) {
+            c->launched = true;
+            c->last_stream = stream;
+        }
         if (e != hipSuccess) {
             free_ctx(c);
             return hip_fail(e, "launch context");

@@ -352,6 +352,10 @@ struct SceneView {
     const MatRec* bmat;     // BVH: shading record of each slot
     int32_t n, n_nodes;
     int32_t n_global, global_first;  // BVH: spheres tested before the tree, their first slot
+    // BVH nodes in the LDS "axis-pair" layout (node_pairs): byte offsets of the y
+    // and z pair arrays and of the child references in the node block.
+    bool pairs;
+    int32_t node_y, node_z, node_refs;
 };
 
 // Scene.Hit (ray/objects.go:37-46) as the reference's linear scan over
@@ -388,6 +392,24 @@ __device__ __forceinline__ float f32_up(double v) {
     float f = (float)v;
     if ((double)f < v) f = __uint_as_float(__float_as_uint(f) + 1u);
     return f;
+}
+
+// BVH nodes in LDS ("axis-pair" layout). The global array is Bvh4Node (128 B,
+// one node's seven 16-B plane blocks together). Staged in LDS it is transposed
+// into [x pairs][y pairs][z pairs][refs]: per node a 32-B (lo, hi) pair per
+// axis and its 16-B reference block, 112 B per node. A ds_read_b128 serves 16
+// lanes per LDS cycle and the bank of byte address a is (a / 4) mod 64, so
+// with 128-B nodes every lane's near-x read fell into one of only four 4-bank
+// windows (node parity x near side): lanes on different nodes of a wave
+// serialised on them. In the pair layout the window is (8 x node + 4 x side)
+// mod 64, sixteen windows, and the reference block's is 4 x node mod 64.
+#ifndef TRAY_NODE_PAIRS
+#define TRAY_NODE_PAIRS 0
+#endif
+constexpr bool kNodePairs = TRAY_NODE_PAIRS != 0 && kBvhWidth == 4;
+constexpr int32_t kPlaneBytes = 4 * kBvhWidth;  // one plane block: one float per child
+__host__ __device__ constexpr size_t node_block_bytes(int32_t n_nodes) {
+    return kNodePairs ? ((size_t)n_nodes * 7 * kPlaneBytes + 31) / 32 * 32 : (size_t)n_nodes * sizeof(Bvh4Node);
 }
 
 // Per-lane traversal state of one Scene.Hit through the exact-culling 4-wide
@@ -517,11 +539,12 @@ __device__ __forceinline__ void trav_begin32(Trav& T, const SceneView& sv, const
     const float oix = (float)org.x * ix, oiy = (float)org.y * iy, oiz = (float)org.z * iz;
     T.ix = ix, T.iy = iy, T.iz = iz;
     T.oix = oix, T.oiy = oiy, T.oiz = oiz;
-    // Bvh4Node::box[a][s]: the near plane is the low one when the ray runs up the axis.
-    constexpr int32_t kPlane = 4 * kBvhWidth;  // bytes of one plane block (one float per child)
+    // The near plane is the low one when the ray runs up the axis; the offsets
+    // are relative to the node's x-pair address (trav_node).
+    constexpr int32_t kPlane = kPlaneBytes;
     T.near_x = ix < 0.0f ? kPlane : 0;
-    T.near_y = 2 * kPlane + (iy < 0.0f ? kPlane : 0);
-    T.near_z = 4 * kPlane + (iz < 0.0f ? kPlane : 0);
+    T.near_y = (sv.pairs ? sv.node_y : 2 * kPlane) + (iy < 0.0f ? kPlane : 0);
+    T.near_z = (sv.pairs ? sv.node_z : 4 * kPlane) + (iz < 0.0f ? kPlane : 0);
     T.tlim = f32_up(T.closest);
 }
 
@@ -546,12 +569,8 @@ __device__ __forceinline__ void stack_push(Trav& T, const Stk& S, uint32_t key) 
 // One cull at most and no further LDS round trip: an entry that is still
 // beyond tlim is visited anyway, which the box tests and the any-order rule
 // make harmless. Returns its reference, or kBvhNone.
-#ifndef TRAY_POP_SENTINEL
-#define TRAY_POP_SENTINEL 1
-#endif
 template <class Stk>
 __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t below) {
-#if TRAY_POP_SENTINEL
     // Slot 0 always holds ~0 (written only by a push at depth 0, from the empty
     // top), so an empty stack pops ~0: key_tn(~0) is NaN (never culled) and
     // ~0 & 0xFFFF is kBvhNone. No emptiness branches: one divergent cull.
@@ -565,20 +584,6 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t be
         if (T.sp == 0 && key_tn(key) > T.tlim) key = ~0u;
     }
     return key & 0xFFFFu;
-#else
-    if (T.sp == 0) return kBvhNone;
-    uint32_t key = T.top;
-    --T.sp;
-    T.top = below;
-    if (key_tn(key) > T.tlim) {
-        if (T.sp == 0) return kBvhNone;
-        key = T.top;
-        --T.sp;
-        T.top = stack_load(S, T.sp);  // the entry of depth sp sits in slot sp
-        if (T.sp == 0 && key_tn(key) > T.tlim) return kBvhNone;
-    }
-    return key & 0xFFFFu;
-#endif
 }
 
 
@@ -587,8 +592,10 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t be
 // becomes the next reference (the lane's state).
 template <class Stk>
 __device__ __forceinline__ void trav_node(Trav& T, const SceneView& sv, const Stk& S, uint32_t& tested) {
-    constexpr int32_t kPlane = 4 * kBvhWidth;  // far plane block = near ^ kPlane
-    const char* nb = reinterpret_cast<const char*>(sv.nodes + T.cur);
+    constexpr int32_t kPlane = kPlaneBytes;  // far plane block = near ^ kPlane (pairs are 2 x kPlane aligned)
+    const char* const base = reinterpret_cast<const char*>(sv.nodes);
+    const char* nb = base + T.cur * (sv.pairs ? 2u * kPlane : (uint32_t)sizeof(Bvh4Node));
+    const char* rb = sv.pairs ? base + sv.node_refs + T.cur * (uint32_t)kPlane : nb + 6 * kPlane;
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for a pop
     // Hit children: upper 16 bits of the entry distance | reference (tn >= 0, so
     // the keys order like the distances, to bf16 precision); anything else ~0.
@@ -603,7 +610,7 @@ __device__ __forceinline__ void trav_node(Trav& T, const SceneView& sv, const St
         const float4 fy = *reinterpret_cast<const float4*>(nb + (T.near_y ^ kPlane) + 16 * g);
         const float4 nz = *reinterpret_cast<const float4*>(nb + T.near_z + 16 * g);
         const float4 fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ kPlane) + 16 * g);
-        const uint4 rf = *reinterpret_cast<const uint4*>(nb + 6 * kPlane + 16 * g);
+        const uint4 rf = *reinterpret_cast<const uint4*>(rb + 16 * g);
         const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
         const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
         const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
@@ -809,6 +816,9 @@ template <bool kStats, bool kAcc>
 __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st,
                                          const AccCtx& acc) {
     if constexpr (kAcc) {
+#ifdef TRAY_PROBE_NO_ACC_ADD  // diagnostic only (wrong frames): what the LDS adds cost
+        if (color.x != 12345.0) return void(L.busy = false);
+#endif
         LdsF64* s = acc.slabs + (L.slot * kAccCopies + (threadIdx.x % kAccCopies)) * 3u;
         __hip_atomic_fetch_add(s + 0, __builtin_rint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(s + 1, __builtin_rint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -929,12 +939,6 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
 // Written for a wave of lanes on different branches: the work several branches
 // need is done once, before them — the bounce's Philox block and the unit
 // direction (sky, Metal, Dielectric).
-#ifndef TRAY_EARLY_MAT
-#define TRAY_EARLY_MAT 1
-#endif
-#ifndef TRAY_LAZY_UD
-#define TRAY_LAZY_UD 1
-#endif
 template <bool kStats, bool kAcc, typename GeoAt, typename MatAt>
 __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
                                            double dir_lsq, GeoAt geo_at, MatAt mat_at, Stats& st, const AccCtx& acc) {
@@ -943,34 +947,24 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     // (RayColor(depth 0) is black), so no scatter is computed for it.
     const bool last = L.bounce + 1u >= (uint32_t)p.max_depth;
     bool ends = !hit || last;
-#if TRAY_EARLY_MAT
     // Issued first, for every lane (a miss reads a valid record it ignores), so
     // the L2 round trip of the shading record overlaps the FP64 work below
     // instead of starting after it inside the hit branch.
     const double4 g = geo_at();
     const MatRec m = mat_at();
-#endif
     const Block w = philox4x32_10(uni_seed(uni), L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
     const double u0 = uniform(w.x0);
-#if TRAY_LAZY_UD
     // Unit(r.Direction) is read by the sky, Metal and Dielectric, not by Lambertian
     // (nor a last-level hit): a wave whose shading lanes are all Lambertian hits
     // (a camera-ray pass of a diffuse pixel) skips the sqrt and three quotients.
     D3 ud = d3(0, 0, 0);
-    if (!hit || (!last && m.type != kLambertian)) ud = unit_lsq(L.dir, dir_lsq);
-#else
-    const D3 ud = unit_lsq(L.dir, dir_lsq);  // dir_lsq = length_sq(L.dir), the segment's `a`
-#endif
+    if (!hit || (!last && m.type != kLambertian)) ud = unit_lsq(L.dir, dir_lsq);  // dir_lsq = length_sq(L.dir)
     D3 color = d3(0, 0, 0);
     if (!hit) {  // AmbientLight.Hit (ray/objects.go:68-73)
         const double t = 0.5 * (ud.y + 1.0);
         const D3 bg_a = d3(uni->bg_a.x, uni->bg_a.y, uni->bg_a.z), bg_b = d3(uni->bg_b.x, uni->bg_b.y, uni->bg_b.z);
         color = mul(L.thr, add(smul(bg_a, 1.0 - t), smul(bg_b, t)));
     } else if (!last) {
-#if !TRAY_EARLY_MAT
-        const double4 g = geo_at();
-        const MatRec m = mat_at();
-#endif
         const D3 point = add(L.org, smul(L.dir, closest));                             // Ray.At (ray/ray.go:23-25)
         const D3 outward = sdiv_rcp(sub(point, d3(g.x, g.y, g.z)), m.radius, m.rinv);  // ray/objects.go:100
         const bool front = dot(L.dir, outward) < 0;                                    // SetFaceNormal (:19-26)
@@ -1013,12 +1007,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     // Settle the shading-record loads here, on every path: vmcnt is one in-order
     // counter, so a load still pending when end_path stores would make the next
     // write of its registers wait for the stores' write-back too.
-#ifndef TRAY_SHADE_SETTLE
-#define TRAY_SHADE_SETTLE 1
-#endif
-#if TRAY_SHADE_SETTLE
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#endif
     if (!ends) return true;
     end_path<kStats, kAcc>(p, L, color, st, acc);
     return false;
@@ -1074,14 +1063,6 @@ constexpr int32_t kDeepNodes = 384;
 // dense scenes) issue ahead of other waves' VALU work, and their latency hides
 // behind it (C2 -0.30 %, C5 -0.39 %; levels 1-3 alike; raising it instead for the
 // node steps, the camera rays or the shading phase gained nothing or lost).
-#ifndef TRAY_PRIO_LEAF
-#define TRAY_PRIO_LEAF 1
-#endif
-// Camera rays answered by their candidate list are shaded inside the refill phase (1) or wait for
-// the shade phase (0).
-#ifndef TRAY_REFILL_SHADE
-#define TRAY_REFILL_SHADE 1
-#endif
 
 // Cost probes (diagnostic builds only, never timed as the product): N extra
 // independent VALU instructions in one phase, to measure what an instruction
@@ -1183,6 +1164,31 @@ __device__ __forceinline__ void prof_material(int site, bool active, int32_t slo
 // wave's slowest ray: it shades and starts its next segment while others still
 // traverse.
 
+// Copies the BVH nodes into LDS at `dst` (node_block_bytes(p.n_nodes) bytes) and
+// sets the scene view's layout fields: the axis-pair layout (kNodePairs), else
+// the global Bvh4Node array as it is.
+__device__ __forceinline__ void stage_nodes(const KernelParams& p, double4* dst, SceneView& sv) {
+    const float4* gn = reinterpret_cast<const float4*>(p.nodes);  // 16-B blocks, 8 per node
+    float4* d = reinterpret_cast<float4*>(dst);
+    const uint32_t n = (uint32_t)p.n_nodes;
+    if constexpr (kNodePairs) {
+        // block c of node i (c = 2 axis + side; c = 6 the references) -> its pair array
+        for (uint32_t k = threadIdx.x; k < 7u * n; k += blockDim.x) {
+            const uint32_t i = k / 7u, c = k - 7u * i;
+            const uint32_t at = c < 6u ? (c >> 1) * 2u * n + 2u * i + (c & 1u) : 6u * n + i;
+            d[at] = gn[8u * i + c];
+        }
+        sv.pairs = true;
+        sv.node_y = (int32_t)(2u * n * kPlaneBytes);
+        sv.node_z = (int32_t)(4u * n * kPlaneBytes);
+        sv.node_refs = (int32_t)(6u * n * kPlaneBytes);
+    } else {
+        const uint32_t n16 = n * (uint32_t)(sizeof(Bvh4Node) / 16);
+        for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) d[k] = gn[k];
+    }
+    sv.nodes = reinterpret_cast<const Bvh4Node*>(dst);
+}
+
 // LDS bytes of `slots` stack slots of a BVH workgroup (32-bit entries).
 __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (size_t)slots * kStackSlotBytes; }
 
@@ -1220,7 +1226,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     }
     const UniPtr uni = uni_lds;
     SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single != 0,       p.bgeo, p.bidx,
-                 p.bmat, p.n,     p.n_nodes,   p.n_global, p.n_slots - p.n_global};
+                 p.bmat, p.n,     p.n_nodes,   p.n_global, p.n_slots - p.n_global, false, 0, 0, 0};
     Stack<kSpill> S{nullptr, nullptr, 0, 0};
     if constexpr (kBVH) {
         // [stacks: stack_cap x blockDim x 4 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]
@@ -1233,18 +1239,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         double4* scene = smem + bvh_stack_bytes(p.stack_lds) / sizeof(double4);
         if constexpr (kLDS == 1) {
             double4* lds_nodes = scene;
-            double4* lds_geo = scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4));
+            double4* lds_geo = scene + node_block_bytes(p.n_nodes) / sizeof(double4);
             int32_t* lds_idx = reinterpret_cast<int32_t*>(lds_geo + p.n_slots);
             int32_t* lds_leaves = lds_idx + p.n_slots;
-            const double4* gn = reinterpret_cast<const double4*>(p.nodes);
-            const int n4 = p.n_nodes * (int)(sizeof(Bvh4Node) / sizeof(double4));
-            for (int i = threadIdx.x; i < n4; i += blockDim.x) lds_nodes[i] = gn[i];
+            stage_nodes(p, lds_nodes, sv);
             for (int i = threadIdx.x; i < p.n_slots; i += blockDim.x) {
                 lds_geo[i] = p.bgeo[i];
                 lds_idx[i] = p.bidx[i];
             }
             for (int i = threadIdx.x; i < p.n_leaves; i += blockDim.x) lds_leaves[i] = p.leaves[i];
-            sv.nodes = reinterpret_cast<const Bvh4Node*>(lds_nodes);
             sv.bgeo = lds_geo;
             sv.bidx = lds_idx;
             sv.leaves = lds_leaves;
@@ -1252,13 +1255,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             // [nodes][leaves]: the traversal's dependent loads stay on chip; each
             // leaf's sphere is one 32-B global load (L2-resident).
             double4* lds_nodes = scene;
-            int32_t* lds_leaves =
-                reinterpret_cast<int32_t*>(scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4)));
-            const double4* gn = reinterpret_cast<const double4*>(p.nodes);
-            const int n4 = p.n_nodes * (int)(sizeof(Bvh4Node) / sizeof(double4));
-            for (int i = threadIdx.x; i < n4; i += blockDim.x) lds_nodes[i] = gn[i];
+            int32_t* lds_leaves = reinterpret_cast<int32_t*>(scene + node_block_bytes(p.n_nodes) / sizeof(double4));
+            stage_nodes(p, lds_nodes, sv);
             for (int i = threadIdx.x; i < p.n_leaves; i += blockDim.x) lds_leaves[i] = p.leaves[i];
-            sv.nodes = reinterpret_cast<const Bvh4Node*>(lds_nodes);
             sv.leaves = lds_leaves;
         }
     } else if constexpr (kLDS == 1) {
@@ -1451,7 +1450,6 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #ifdef TRAY_PROFILE_REFILL
         const uint64_t prof_shade0 = __builtin_amdgcn_s_memtime();
 #endif
-#if TRAY_REFILL_SHADE
         // The refill's camera rays with a known hit are shaded at once (their
         // scattered rays join the node steps below) instead of waiting for the
         // shade batch; the traversal lanes' batching is unchanged.
@@ -1473,9 +1471,6 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
             }
         }
-#else
-        (void)cam_hit;
-#endif
 #ifdef TRAY_PROFILE_REFILL
         {
             const uint64_t prof_shade1 = __builtin_amdgcn_s_memtime();
@@ -1572,9 +1567,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 TRAY_MARK("leaf_ctl")
                 PROF_CNT(6, 1);
                 PROF_CNT(7, __popcll(m_leaf));
-#if TRAY_PRIO_LEAF
-                __builtin_amdgcn_s_setprio(TRAY_PRIO_LEAF);
-#endif
+                __builtin_amdgcn_s_setprio(1);
                 if (is_leaf(T.cur)) {
                     TRAY_MARK("leaf")
                     uint32_t tested;
@@ -1598,9 +1591,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #endif
                 }
                 PROF_ADD(2);
-#if TRAY_PRIO_LEAF
                 __builtin_amdgcn_s_setprio(0);
-#endif
             }
             // Shading phase, batched.
             const uint64_t m_shade = __ballot(L.busy && T.cur == kBvhNone);
@@ -2032,14 +2023,14 @@ static int resident_blocks(int device, KernelFn fn, int threads, size_t lds) {
 
 // Scene bytes staged in LDS (nodes, geometry, indices, leaf table), 16-B aligned.
 static size_t scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves) {
-    const size_t b = (size_t)n_nodes * sizeof(Bvh4Node) + (size_t)n_slots * (sizeof(double4) + sizeof(int32_t)) +
+    const size_t b = node_block_bytes(n_nodes) + (size_t)n_slots * (sizeof(double4) + sizeof(int32_t)) +
                      (size_t)n_leaves * sizeof(int32_t);
     return (b + 15) / 16 * 16;
 }
 
 // The nodes-only layout (kLDS 2): nodes and leaf table.
 static size_t nodes_lds_bytes(int32_t n_nodes, int32_t n_leaves) {
-    return ((size_t)n_nodes * sizeof(Bvh4Node) + (size_t)n_leaves * sizeof(int32_t) + 15) / 16 * 16;
+    return (node_block_bytes(n_nodes) + (size_t)n_leaves * sizeof(int32_t) + 15) / 16 * 16;
 }
 
 size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap) {
