@@ -59,5 +59,11 @@ struct Bvh {
 // Returns false on non-finite input or a tree the kernel cannot index (the
 // caller then uses the linear scan).
 bool build_bvh(const tray_sphere* spheres, int32_t n, Bvh* out, int leaf_max = 1);
+// Build variants for offline comparison (tools/bvh_sim.cpp); the defaults are build_bvh's.
+struct BvhOptions {
+    bool sweep = false;  // full-sweep SAH instead of 32 bins
+    int collapse = 0;    // 0: open the largest-area child; 1: the largest area x primitive count
+};
+bool build_bvh_opts(const tray_sphere* spheres, int32_t n, Bvh* out, int leaf_max, const BvhOptions& opt);
 
 }  // namespace tray

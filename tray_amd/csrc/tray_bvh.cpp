@@ -81,6 +81,7 @@ struct Builder {
     double pad = 0;
     int leaf_max = 1;
     int32_t stack_max = 0;
+    BvhOptions opt;
 
     static float down(double v) {
         float f = (float)v;
@@ -114,6 +115,7 @@ struct Builder {
 
     // Binned SAH over centroids; object median when deep or degenerate.
     int split(int b, int e, int depth) {
+        if (opt.sweep) return split_sweep(b, e, depth);
         constexpr int kBins = 32;
         double cmin[3], cmax[3];
         for (int k = 0; k < 3; ++k) {
@@ -200,6 +202,71 @@ struct Builder {
         return mid;
     }
 
+    // Full-sweep SAH (tools/bvh_sim): every split between consecutive centroids
+    // along each axis (ties in list order), cost A_L N_L + A_R N_R.
+    int split_sweep(int b, int e, int depth) {
+        const int n = e - b;
+        double best = INFINITY;
+        int best_axis = -1, best_at = -1;
+        std::vector<Prim> tmp(prims.begin() + b, prims.begin() + e);
+        std::vector<double> right(n + 1);
+        for (int k = 0; k < 3 && depth < kSahDepth; ++k) {
+            std::stable_sort(tmp.begin(), tmp.end(), [k](const Prim& x, const Prim& y) { return x.c[k] < y.c[k]; });
+            Box acc;
+            for (int i = n - 1; i >= 1; --i) {
+                acc.grow(tmp[i].box);
+                right[i] = acc.area() * (n - i);
+            }
+            Box left;
+            for (int i = 1; i < n; ++i) {
+                left.grow(tmp[i - 1].box);
+                if (tmp[i].c[k] == tmp[i - 1].c[k]) continue;  // no plane between equal centroids
+                const double cost = left.area() * i + right[i];
+                if (cost < best) {
+                    best = cost;
+                    best_axis = k;
+                    best_at = i;
+                }
+            }
+        }
+        if (best_axis < 0) {
+            const int mid = b + n / 2;
+            int k = 0;
+            double ext[3];
+            for (int a = 0; a < 3; ++a) {
+                double lo = INFINITY, hi = -INFINITY;
+                for (int i = b; i < e; ++i) lo = std::min(lo, prims[i].c[a]), hi = std::max(hi, prims[i].c[a]);
+                ext[a] = hi - lo;
+            }
+            for (int a = 1; a < 3; ++a)
+                if (ext[a] > ext[k]) k = a;
+            std::stable_sort(prims.begin() + b, prims.begin() + e, [k](const Prim& x, const Prim& y) { return x.c[k] < y.c[k]; });
+            const auto by_index = [](const Prim& x, const Prim& y) { return x.index < y.index; };
+            std::sort(prims.begin() + b, prims.begin() + mid, by_index);
+            std::sort(prims.begin() + mid, prims.begin() + e, by_index);
+            return mid;
+        }
+        const int k = best_axis;
+        std::stable_sort(tmp.begin(), tmp.end(), [k](const Prim& x, const Prim& y) { return x.c[k] < y.c[k]; });
+        const auto by_index = [](const Prim& x, const Prim& y) { return x.index < y.index; };
+        std::sort(tmp.begin(), tmp.begin() + best_at, by_index);
+        std::sort(tmp.begin() + best_at, tmp.end(), by_index);
+        std::copy(tmp.begin(), tmp.end(), prims.begin() + b);
+        return b + best_at;
+    }
+
+    // Which inner child the collapse opens next (opt.collapse): 0 the largest
+    // area, 1 the largest area x primitive count.
+    double open_score(int c) const {
+        const double a = bin[c].box.area();
+        if (opt.collapse == 1) return a * (double)count_of(c);
+        return a;
+    }
+    int count_of(int c) const {
+        if (bin[c].count > 0) return bin[c].count;
+        return count_of(bin[c].left) + count_of(bin[c].right);
+    }
+
     // Emit the 4-wide node for binary inner node `n` (pre-order); `depth_stack`
     // = stack entries its ancestors may have left. Returns the node index.
     int collapse(int n, int32_t depth_stack, const tray_sphere* s) {
@@ -209,9 +276,9 @@ struct Builder {
             int pick = -1;
             double pick_area = -1;
             for (int k = 0; k < cnt; ++k)
-                if (bin[ch[k]].count == 0 && bin[ch[k]].box.area() > pick_area) {
+                if (bin[ch[k]].count == 0 && open_score(ch[k]) > pick_area) {
                     pick = k;
-                    pick_area = bin[ch[k]].box.area();
+                    pick_area = open_score(ch[k]);
                 }
             if (pick < 0) break;
             const int c = ch[pick];
@@ -258,6 +325,10 @@ struct Builder {
 }  // namespace
 
 bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
+    return build_bvh_opts(s, n, out, leaf_max, BvhOptions{});
+}
+
+bool build_bvh_opts(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max, const BvhOptions& opt) {
     out->nodes.clear();
     out->leaves.clear();
     out->geo.clear();
@@ -267,6 +338,7 @@ bool build_bvh(const tray_sphere* s, int32_t n, Bvh* out, int leaf_max) {
     out->n_global = 0;
     if (n <= 0) return true;
     Builder B;
+    B.opt = opt;
     B.prims.resize((size_t)n);
     double m = 0;
     for (int32_t i = 0; i < n; ++i) {

@@ -352,10 +352,6 @@ struct SceneView {
     const MatRec* bmat;     // BVH: shading record of each slot
     int32_t n, n_nodes;
     int32_t n_global, global_first;  // BVH: spheres tested before the tree, their first slot
-    // BVH nodes in the LDS "axis-pair" layout (node_pairs): byte offsets of the y
-    // and z pair arrays and of the child references in the node block.
-    bool pairs;
-    int32_t node_y, node_z, node_refs;
 };
 
 // Scene.Hit (ray/objects.go:37-46) as the reference's linear scan over
@@ -392,24 +388,6 @@ __device__ __forceinline__ float f32_up(double v) {
     float f = (float)v;
     if ((double)f < v) f = __uint_as_float(__float_as_uint(f) + 1u);
     return f;
-}
-
-// BVH nodes in LDS ("axis-pair" layout). The global array is Bvh4Node (128 B,
-// one node's seven 16-B plane blocks together). Staged in LDS it is transposed
-// into [x pairs][y pairs][z pairs][refs]: per node a 32-B (lo, hi) pair per
-// axis and its 16-B reference block, 112 B per node. A ds_read_b128 serves 16
-// lanes per LDS cycle and the bank of byte address a is (a / 4) mod 64, so
-// with 128-B nodes every lane's near-x read fell into one of only four 4-bank
-// windows (node parity x near side): lanes on different nodes of a wave
-// serialised on them. In the pair layout the window is (8 x node + 4 x side)
-// mod 64, sixteen windows, and the reference block's is 4 x node mod 64.
-#ifndef TRAY_NODE_PAIRS
-#define TRAY_NODE_PAIRS 0
-#endif
-constexpr bool kNodePairs = TRAY_NODE_PAIRS != 0 && kBvhWidth == 4;
-constexpr int32_t kPlaneBytes = 4 * kBvhWidth;  // one plane block: one float per child
-__host__ __device__ constexpr size_t node_block_bytes(int32_t n_nodes) {
-    return kNodePairs ? ((size_t)n_nodes * 7 * kPlaneBytes + 31) / 32 * 32 : (size_t)n_nodes * sizeof(Bvh4Node);
 }
 
 // Per-lane traversal state of one Scene.Hit through the exact-culling 4-wide
@@ -539,12 +517,11 @@ __device__ __forceinline__ void trav_begin32(Trav& T, const SceneView& sv, const
     const float oix = (float)org.x * ix, oiy = (float)org.y * iy, oiz = (float)org.z * iz;
     T.ix = ix, T.iy = iy, T.iz = iz;
     T.oix = oix, T.oiy = oiy, T.oiz = oiz;
-    // The near plane is the low one when the ray runs up the axis; the offsets
-    // are relative to the node's x-pair address (trav_node).
-    constexpr int32_t kPlane = kPlaneBytes;
+    // Bvh4Node::box[a][s]: the near plane is the low one when the ray runs up the axis.
+    constexpr int32_t kPlane = 4 * kBvhWidth;  // bytes of one plane block (one float per child)
     T.near_x = ix < 0.0f ? kPlane : 0;
-    T.near_y = (sv.pairs ? sv.node_y : 2 * kPlane) + (iy < 0.0f ? kPlane : 0);
-    T.near_z = (sv.pairs ? sv.node_z : 4 * kPlane) + (iz < 0.0f ? kPlane : 0);
+    T.near_y = 2 * kPlane + (iy < 0.0f ? kPlane : 0);
+    T.near_z = 4 * kPlane + (iz < 0.0f ? kPlane : 0);
     T.tlim = f32_up(T.closest);
 }
 
@@ -592,10 +569,8 @@ __device__ __forceinline__ uint32_t stack_pop(Trav& T, const Stk& S, uint32_t be
 // becomes the next reference (the lane's state).
 template <class Stk>
 __device__ __forceinline__ void trav_node(Trav& T, const SceneView& sv, const Stk& S, uint32_t& tested) {
-    constexpr int32_t kPlane = kPlaneBytes;  // far plane block = near ^ kPlane (pairs are 2 x kPlane aligned)
-    const char* const base = reinterpret_cast<const char*>(sv.nodes);
-    const char* nb = base + T.cur * (sv.pairs ? 2u * kPlane : (uint32_t)sizeof(Bvh4Node));
-    const char* rb = sv.pairs ? base + sv.node_refs + T.cur * (uint32_t)kPlane : nb + 6 * kPlane;
+    constexpr int32_t kPlane = 4 * kBvhWidth;  // far plane block = near ^ kPlane
+    const char* nb = reinterpret_cast<const char*>(sv.nodes + T.cur);
     const uint32_t below = stack_load(S, max(T.sp - 1, 0));  // read ahead for a pop
     // Hit children: upper 16 bits of the entry distance | reference (tn >= 0, so
     // the keys order like the distances, to bf16 precision); anything else ~0.
@@ -610,7 +585,7 @@ __device__ __forceinline__ void trav_node(Trav& T, const SceneView& sv, const St
         const float4 fy = *reinterpret_cast<const float4*>(nb + (T.near_y ^ kPlane) + 16 * g);
         const float4 nz = *reinterpret_cast<const float4*>(nb + T.near_z + 16 * g);
         const float4 fz = *reinterpret_cast<const float4*>(nb + (T.near_z ^ kPlane) + 16 * g);
-        const uint4 rf = *reinterpret_cast<const uint4*>(rb + 16 * g);
+        const uint4 rf = *reinterpret_cast<const uint4*>(nb + 6 * kPlane + 16 * g);
         const uint32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
         const float nxa[4] = {nx.x, nx.y, nx.z, nx.w}, fxa[4] = {fx.x, fx.y, fx.z, fx.w};
         const float nya[4] = {ny.x, ny.y, ny.z, ny.w}, fya[4] = {fy.x, fy.y, fy.z, fy.w};
@@ -1164,31 +1139,6 @@ __device__ __forceinline__ void prof_material(int site, bool active, int32_t slo
 // wave's slowest ray: it shades and starts its next segment while others still
 // traverse.
 
-// Copies the BVH nodes into LDS at `dst` (node_block_bytes(p.n_nodes) bytes) and
-// sets the scene view's layout fields: the axis-pair layout (kNodePairs), else
-// the global Bvh4Node array as it is.
-__device__ __forceinline__ void stage_nodes(const KernelParams& p, double4* dst, SceneView& sv) {
-    const float4* gn = reinterpret_cast<const float4*>(p.nodes);  // 16-B blocks, 8 per node
-    float4* d = reinterpret_cast<float4*>(dst);
-    const uint32_t n = (uint32_t)p.n_nodes;
-    if constexpr (kNodePairs) {
-        // block c of node i (c = 2 axis + side; c = 6 the references) -> its pair array
-        for (uint32_t k = threadIdx.x; k < 7u * n; k += blockDim.x) {
-            const uint32_t i = k / 7u, c = k - 7u * i;
-            const uint32_t at = c < 6u ? (c >> 1) * 2u * n + 2u * i + (c & 1u) : 6u * n + i;
-            d[at] = gn[8u * i + c];
-        }
-        sv.pairs = true;
-        sv.node_y = (int32_t)(2u * n * kPlaneBytes);
-        sv.node_z = (int32_t)(4u * n * kPlaneBytes);
-        sv.node_refs = (int32_t)(6u * n * kPlaneBytes);
-    } else {
-        const uint32_t n16 = n * (uint32_t)(sizeof(Bvh4Node) / 16);
-        for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) d[k] = gn[k];
-    }
-    sv.nodes = reinterpret_cast<const Bvh4Node*>(dst);
-}
-
 // LDS bytes of `slots` stack slots of a BVH workgroup (32-bit entries).
 __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (size_t)slots * kStackSlotBytes; }
 
@@ -1226,7 +1176,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     }
     const UniPtr uni = uni_lds;
     SceneView sv{p.geo,  p.nodes, p.leaves,    p.leaf_single != 0,       p.bgeo, p.bidx,
-                 p.bmat, p.n,     p.n_nodes,   p.n_global, p.n_slots - p.n_global, false, 0, 0, 0};
+                 p.bmat, p.n,     p.n_nodes,   p.n_global, p.n_slots - p.n_global};
     Stack<kSpill> S{nullptr, nullptr, 0, 0};
     if constexpr (kBVH) {
         // [stacks: stack_cap x blockDim x 4 B][nodes: n_nodes x 128 B][bgeo: n_slots x 32 B]
@@ -1239,15 +1189,18 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         double4* scene = smem + bvh_stack_bytes(p.stack_lds) / sizeof(double4);
         if constexpr (kLDS == 1) {
             double4* lds_nodes = scene;
-            double4* lds_geo = scene + node_block_bytes(p.n_nodes) / sizeof(double4);
+            double4* lds_geo = scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4));
             int32_t* lds_idx = reinterpret_cast<int32_t*>(lds_geo + p.n_slots);
             int32_t* lds_leaves = lds_idx + p.n_slots;
-            stage_nodes(p, lds_nodes, sv);
+            const double4* gn = reinterpret_cast<const double4*>(p.nodes);
+            const int n4 = p.n_nodes * (int)(sizeof(Bvh4Node) / sizeof(double4));
+            for (int i = threadIdx.x; i < n4; i += blockDim.x) lds_nodes[i] = gn[i];
             for (int i = threadIdx.x; i < p.n_slots; i += blockDim.x) {
                 lds_geo[i] = p.bgeo[i];
                 lds_idx[i] = p.bidx[i];
             }
             for (int i = threadIdx.x; i < p.n_leaves; i += blockDim.x) lds_leaves[i] = p.leaves[i];
+            sv.nodes = reinterpret_cast<const Bvh4Node*>(lds_nodes);
             sv.bgeo = lds_geo;
             sv.bidx = lds_idx;
             sv.leaves = lds_leaves;
@@ -1255,9 +1208,13 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             // [nodes][leaves]: the traversal's dependent loads stay on chip; each
             // leaf's sphere is one 32-B global load (L2-resident).
             double4* lds_nodes = scene;
-            int32_t* lds_leaves = reinterpret_cast<int32_t*>(scene + node_block_bytes(p.n_nodes) / sizeof(double4));
-            stage_nodes(p, lds_nodes, sv);
+            int32_t* lds_leaves =
+                reinterpret_cast<int32_t*>(scene + (size_t)p.n_nodes * (sizeof(Bvh4Node) / sizeof(double4)));
+            const double4* gn = reinterpret_cast<const double4*>(p.nodes);
+            const int n4 = p.n_nodes * (int)(sizeof(Bvh4Node) / sizeof(double4));
+            for (int i = threadIdx.x; i < n4; i += blockDim.x) lds_nodes[i] = gn[i];
             for (int i = threadIdx.x; i < p.n_leaves; i += blockDim.x) lds_leaves[i] = p.leaves[i];
+            sv.nodes = reinterpret_cast<const Bvh4Node*>(lds_nodes);
             sv.leaves = lds_leaves;
         }
     } else if constexpr (kLDS == 1) {
@@ -2023,14 +1980,14 @@ static int resident_blocks(int device, KernelFn fn, int threads, size_t lds) {
 
 // Scene bytes staged in LDS (nodes, geometry, indices, leaf table), 16-B aligned.
 static size_t scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves) {
-    const size_t b = node_block_bytes(n_nodes) + (size_t)n_slots * (sizeof(double4) + sizeof(int32_t)) +
+    const size_t b = (size_t)n_nodes * sizeof(Bvh4Node) + (size_t)n_slots * (sizeof(double4) + sizeof(int32_t)) +
                      (size_t)n_leaves * sizeof(int32_t);
     return (b + 15) / 16 * 16;
 }
 
 // The nodes-only layout (kLDS 2): nodes and leaf table.
 static size_t nodes_lds_bytes(int32_t n_nodes, int32_t n_leaves) {
-    return (node_block_bytes(n_nodes) + (size_t)n_leaves * sizeof(int32_t) + 15) / 16 * 16;
+    return ((size_t)n_nodes * sizeof(Bvh4Node) + (size_t)n_leaves * sizeof(int32_t) + 15) / 16 * 16;
 }
 
 size_t bvh_scene_lds_bytes(int32_t n_nodes, int32_t n_slots, int32_t n_leaves, int32_t stack_cap) {
