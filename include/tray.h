@@ -61,8 +61,7 @@ extern "C" {
 
 #define TRAY_ABI_VERSION 5 /* 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get;
                               4: TRAY_FLAG_ORDERED_SUM (the library no longer reads the process environment);
-                              5: a scene handle may be rendered on several streams at once (launch contexts);
-                                 tray_render_plan.acc_run (accumulator runs of up to 4 chunks at r >= 128) */
+                              5: a scene handle may be rendered on several streams at once (launch contexts) */
 
 typedef enum tray_status {
     TRAY_OK = 0,
@@ -316,9 +315,7 @@ typedef struct tray_render_plan {
     int32_t bvh;               /* 1: the BVH kernel; 0: the reference-order linear scan */
     int32_t lds_layout;        /* BVH: as tray_scene_info.lds_resident; linear scan: 1 geometry in LDS */
     int32_t stack_lds;         /* BVH: traversal stack entries per lane kept in LDS */
-    int32_t acc_run;           /* fixed point: consecutive 64-sample chunks of a pixel-pass summed in one exact
-                                  accumulator (1..4; each sample then has 47 - log2(acc_run) bits, which sets k),
-                                  one buffer record per run (ABI 5; was reserved, 0) */
+    int32_t reserved;          /* 0 */
     int64_t lds_bytes;         /* dynamic LDS per workgroup */
     int64_t buffer_bytes;      /* device workspace for the samples or chunk records of one launch band */
 } tray_render_plan;

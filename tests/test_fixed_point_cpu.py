@@ -65,55 +65,3 @@ def test_nan_sample_poisons_its_channel():
     v = np.rint(np.ldexp(np.linspace(0, 0.5, 64), 46))
     v[17] = np.nan
     assert math.isnan(chunk_sum(v, range(64), 2))
-
-
-def fixed_point(bound, spp, run_log2_max=2, bits=K_BITS, min_shift=44):
-    """tray_abi.hip fixed_point(): (k, run) for a colour bound C and r = spp: the
-    longest run of 64-sample chunks (<= 2^run_log2_max, <= the pixel-pass's
-    chunks) whose samples, given bits - log2(run) bits each, still leave
-    k = bits - log2(run) - e >= min_shift (C < 2^e); (0, 1) when none does."""
-    if spp % 64 or not bound < 2.0 ** 20:
-        return 0, 1
-    e = math.frexp(max(bound, 2.0 ** -300))[1]
-    for lg in range(run_log2_max, -1, -1):
-        if (1 << lg) > spp // 64:
-            continue
-        k = bits - lg - e
-        if k >= min_shift:
-            return min(k, 600), 1 << lg
-    return 0, 1
-
-
-@pytest.mark.parametrize("spp", [64, 128, 192, 256, 1024])
-def test_accumulator_runs_are_exact(spp):
-    """r >= 128 (C3/C4/C5): one accumulator holds a run of up to 4 consecutive
-    chunks of a pixel-pass, so its sum has up to 256 terms: with k reduced by
-    log2(run) every term is <= 2^(47 - log2 run) and the run's sum is an exact
-    FP64 integer in any order and split, the same as per-chunk sums added as
-    int64 (the resolve walks a pixel-pass's runs). The book-cover bound 1.001
-    gives k = 46 at r = 64 and 44 with runs of 4 (the C3/C5 plans)."""
-    rng = np.random.default_rng(spp)
-    k, run = fixed_point(1.001, spp)
-    assert (k, run) == ((46, 1) if spp == 64 else (45, 2) if spp in (128, 192) else (44, 4))
-    c = rng.uniform(0, 1.0, spp)
-    v = np.rint(np.ldexp(c, k))
-    assert np.max(np.abs(v)) * 64 * run <= 2.0 ** 53
-    per_chunk = [int(chunk_sum(v[i:i + 64], rng.permutation(64), 2)) for i in range(0, spp, 64)]
-    runs = []
-    i = 0
-    while i < spp // 64:  # runs never cross the pixel-pass; a late single-chunk take may cut one short
-        n = min(run, spp // 64 - i, int(rng.integers(1, run + 1)))
-        seg = v[64 * i:64 * (i + n)]
-        runs.append(chunk_sum(seg, rng.permutation(len(seg)), 2))
-        assert runs[-1] == math.fsum(seg)  # exact
-        i += n
-    assert sum(int(x) for x in runs) == sum(per_chunk) == sum(int(x) for x in v)
-
-
-def test_run_choice_falls_back_to_shorter_runs():
-    """A larger colour bound (albedo above 1 over many bounces) leaves fewer bits:
-    the host shortens the runs before giving up the fixed-point sum."""
-    assert fixed_point(3.0, 256) == (44, 2)   # C < 2^2: runs of 4 would leave k = 43
-    assert fixed_point(4.5, 256) == (44, 1)   # C < 2^3: single chunks only
-    assert fixed_point(8.1, 256) == (0, 1)    # C < 2^4: the FP64 sum in sample order
-    assert fixed_point(1.001, 64) == (46, 1) and fixed_point(1.001, 96) == (0, 1)

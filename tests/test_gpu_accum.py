@@ -134,14 +134,9 @@ def test_render_plan(L, O):
             dev.release()
     assert plans["c1"]["fixed_point_shift"] == 0 and plans["c1"]["acc_slots"] == 0
     for c in ("c2", "c5"):
-        assert plans[c]["acc_slots"] >= 8 and plans[c]["bvh"] == 1, plans[c]
-    # C2 (r = 64): one chunk per pixel-pass, k = 46; C5 (r = 256): runs of 4 chunks, k = 44
-    assert (plans["c2"]["fixed_point_shift"], plans["c2"]["acc_run"]) == (46, 1), plans["c2"]
-    assert (plans["c5"]["fixed_point_shift"], plans["c5"]["acc_run"]) == (44, 4), plans["c5"]
-    assert plans["c1"]["acc_run"] == 0
+        assert plans[c]["fixed_point_shift"] == 46 and plans[c]["acc_slots"] >= 8 and plans[c]["bvh"] == 1, plans[c]
     assert plans["c2"]["lds_layout"] == 1 and plans["c5"]["lds_layout"] == 2
-    # C2, 16 frames: one band, one 32-B record per 64 samples (the buffer keeps a record per chunk at
-    # every r: a run's record sits at its first chunk)
+    # C2, 16 frames: one band, one 32-B record per 64 samples
     assert plans["c2"]["buffer_bytes"] == 1280 * 720 * 64 * 16 // 64 * 32
     assert plans["c2"]["lds_bytes"] <= 160 * 1024
 
@@ -187,34 +182,3 @@ def test_environment_is_ignored(L, O):
         os.environ.clear()
         os.environ.update(old)
         dev.release()
-
-
-@pytest.mark.parametrize("spp", [128, 256, 320])
-def test_accumulator_runs_are_invisible(L, O, knobs, spp):
-    """r >= 128: an accumulator holds a run of up to 4 consecutive chunks of a
-    pixel-pass (one record per run, tray_kernel.hpp AccPartial). Runs are cut
-    by single-chunk takes (knob wave_chunks=1: one record per chunk), by
-    reservations of 3 chunks (runs straddle reservation ends), by few slots and
-    by progressive passes in one launch: every frame is bit-identical, and
-    within the parity bar of the oracle."""
-    import torch
-
-    from test_gpu_parity import _passes
-
-    sc = O.rich_scene(2)
-    w, h = 29, 19
-    st = camera(L, RICH_SETUP, w, h)
-    dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
-    try:
-        p = L.make_params(w, h, 50, spp, 0.5, 7, pass_=2)
-        assert dev.plan(st, p, 3).acc_run == (2 if spp == 128 else 4)
-        base = _passes(L, dev, st, p, 3, torch.float64, (h, w, 3))
-        for kn in (dict(wave_chunks=1), dict(wave_chunks=3), dict(acc_slots=2), dict(acc_slots=0)):
-            knobs(**kn)
-            got = _passes(L, dev, st, p, 3, torch.float64, (h, w, 3))
-            assert np.array_equal(got, base), kn
-            L.clear_debug_knobs()
-    finally:
-        dev.release()
-    ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, spp, 50, 0.5, 7, workers=WORKERS, pass_=3)
-    assert float(np.max(np.abs(base[1] - ref))) <= 1e-12

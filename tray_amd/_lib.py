@@ -113,11 +113,11 @@ class SceneInfo(ctypes.Structure):
 class RenderPlan(ctypes.Structure):
     """tray_render_plan: how a render would run (pixel sums, kernel, LDS, workspace)."""
     _fields_ = [("fixed_point_shift", ctypes.c_int32), ("acc_slots", ctypes.c_int32), ("bvh", ctypes.c_int32),
-                ("lds_layout", ctypes.c_int32), ("stack_lds", ctypes.c_int32), ("acc_run", ctypes.c_int32),
+                ("lds_layout", ctypes.c_int32), ("stack_lds", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("lds_bytes", ctypes.c_int64), ("buffer_bytes", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
-        return {name: int(getattr(self, name)) for name, _ in self._fields_}
+        return {name: int(getattr(self, name)) for name, _ in self._fields_ if name != "reserved"}
 
 
 class TrayError(RuntimeError):

@@ -523,45 +523,30 @@ static bool cand_enabled() {
 }
 
 // The fixed-point scale 2^k of a render (tray_kernel.hpp), or 0 for the FP64
-// sum in sample order, and how many consecutive 64-sample chunks of one
-// pixel-pass an on-chip accumulator may hold (`run`, 1..kAccRunMax: one chunk
-// record per run instead of per chunk). Fixed point needs 64 | rays_per_pixel
-// (a 64-item chunk is then one pixel's samples) and a colour bound that leaves
-// k >= kAccMinShift: a sample's colour is its throughput (a product of
-// <= max_depth attenuations, each <= max_att) times a convex combination of the
-// two background colours, so |c| <= C = max|bg| * max_att^max_depth (x 1.001
-// for rounding). A run's sum of run x 64 integers must stay exact in FP64
-// (<= 2^53), so a sample may use kAccBits - log2(run) bits: k is the largest
-// shift with C * 2^k <= 2^(kAccBits - log2 run), for the longest run (at most
-// the pixel-pass's chunks) that still leaves k >= kAccMinShift.
+// sum in sample order. Fixed point needs 64 | rays_per_pixel (a 64-item chunk is
+// then one pixel's samples) and a colour bound that leaves k >= kAccMinShift:
+// a sample's colour is its throughput (a product of <= max_depth attenuations,
+// each <= max_att) times a convex combination of the two background colours,
+// so |c| <= C = max|bg| * max_att^max_depth (x 1.001 for rounding). k is the
+// largest shift with C * 2^k <= 2^kAccBits (tray_kernel.hpp).
 // TRAY_FLAG_ORDERED_SUM selects the FP64 sum in sample order (include/tray.h).
-struct FixedPoint {
-    int32_t shift;  // k; 0: FP64 sum in sample order
-    int32_t run;    // chunks per accumulator run (1 when 64 samples per pixel-pass)
-};
-static FixedPoint fixed_point(const tray_scene_s* sc, const tray_params* p) {
-    const FixedPoint none{0, 1};
-    if (p->rays_per_pixel % 64 != 0) return none;
-    if (p->flags & TRAY_FLAG_ORDERED_SUM) return none;
+static int32_t fixed_point_shift(const tray_scene_s* sc, const tray_params* p) {
+    if (p->rays_per_pixel % 64 != 0) return 0;
+    if (p->flags & TRAY_FLAG_ORDERED_SUM) return 0;
     double bg = 0.0;
     const double comps[6] = {sc->bg_a.x, sc->bg_a.y, sc->bg_a.z, sc->bg_b.x, sc->bg_b.y, sc->bg_b.z};
     for (double c : comps) {
-        if (!std::isfinite(c)) return none;
+        if (!std::isfinite(c)) return 0;
         bg = std::max(bg, std::fabs(c));
     }
-    if (!std::isfinite(sc->max_att)) return none;
+    if (!std::isfinite(sc->max_att)) return 0;
     const double bound = bg * std::pow(sc->max_att, (double)p->max_depth) * 1.001;
-    if (!(bound < 0x1p20)) return none;
+    if (!(bound < 0x1p20)) return 0;
     int e = 0;
     std::frexp(std::max(bound, 0x1p-300), &e);  // bound < 2^e
-    if (p->rays_per_pixel > (1 << 15)) return none;  // the pixel's total r x 2^47 must stay below 2^63
-    for (int32_t lg = kAccRunLog2Max; lg >= 0; --lg) {
-        const int32_t run = 1 << lg;
-        if (run > p->rays_per_pixel / 64) continue;
-        const int32_t k = kAccBits - lg - e;
-        if (k >= kAccMinShift) return FixedPoint{std::min(k, 600), run};
-    }
-    return none;
+    if (p->rays_per_pixel > (1 << 15)) return 0;  // the pixel's total r x 2^47 must stay below 2^63
+    const int32_t k = kAccBits - e;
+    return k >= kAccMinShift ? std::min(k, 600) : 0;
 }
 
 // The kernel parameters of a render of `p` on `sc` (everything but the output,
@@ -604,9 +589,7 @@ static int prepare_render(tray_scene_t sc, const tray_camera* cam, const tray_pa
     k.cam.aperture = cam->aperture;
     k.bg_a = sc->bg_a;
     k.bg_b = sc->bg_b;
-    const FixedPoint fx = fixed_point(sc, p);
-    k.acc_shift = fx.shift;
-    k.acc_run_max = (uint32_t)fx.run;
+    k.acc_shift = fixed_point_shift(sc, p);
     if (k.acc_shift > 0) {  // the scale rides on the background: every colour is then scaled (exactly)
         for (V3* v : {&k.bg_a, &k.bg_b}) {
             v->x = std::ldexp(v->x, k.acc_shift);
@@ -769,7 +752,6 @@ int tray_render_plan_get(tray_scene_t sc, const tray_camera* cam, const tray_par
     const LaunchPlan plan = plan_launch(k, use_bvh);
     const LaunchLayout& L = plan.layout;
     out->fixed_point_shift = k.acc_shift;
-    out->acc_run = k.acc_shift > 0 ? (int32_t)k.acc_run_max : 0;
     out->acc_slots = L.acc_slots;
     out->bvh = use_bvh ? 1 : 0;
     out->lds_layout = L.lds_mode;

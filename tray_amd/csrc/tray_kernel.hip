@@ -897,11 +897,10 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
             for (int c = 0; c < 3; ++c) sum[c] += v[3 * k + c];
 #pragma unroll
         for (int k = 0; k < 3 * kAccCopies; ++k) v[k] = 0.0;
-        AccPartial* o = reinterpret_cast<AccPartial*>(p.samples) + (chunk_of & kAccChunkMask);
+        AccPartial* o = reinterpret_cast<AccPartial*>(p.samples) + chunk_of;
         o->sum[0] = sum[0];
         o->sum[1] = sum[1];
         o->sum[2] = sum[2];
-        o->chunks = (double)(chunk_of >> kAccRunShift);
     }
     return freed;
 }
@@ -1226,7 +1225,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     AccCtx acc{nullptr};
     uint64_t acc_free = 0;   // kAcc, wave-uniform: free slots
     uint64_t acc_all = 0;    // kAcc, wave-uniform: every slot
-    uint32_t acc_chunk = 0;  // kAcc: lane s holds slot s's first chunk | run length << kAccRunShift
+    uint32_t acc_chunk = 0;  // kAcc: lane s holds the chunk of slot s
     if constexpr (kAcc) {
         LdsF64* all = (LdsF64*)reinterpret_cast<double*>(reinterpret_cast<char*>(smem_all) + p.acc_off);
         const uint32_t waves = blockDim.x / 64u, slots = (uint32_t)p.acc_slots;
@@ -1284,29 +1283,17 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #endif
         while (idle != 0ull && !exhausted) {
             if (pool_next == pool_end) {
-                // kAcc, wave-uniform: the next chunk continues the current chunk's
-                // pixel-pass (the wave's reservation holds it, and it is not a
-                // pass's first chunk) and joins its accumulator run (tray_kernel.hpp).
-                bool join = false;
-                if constexpr (kAcc) {
-                    if (p.acc_run_max > 1u && grp_next < grp_end) {
-                        uint32_t rem;
-                        (void)udiv(grp_next * 64u, p.div_spp, rem);
-                        join = rem != 0u &&
-                               ((uint32_t)__builtin_amdgcn_readlane(acc_chunk, pool_slot) >> kAccRunShift) < p.acc_run_max;
-                    }
-                }
                 if constexpr (kAcc) {
                     // A chunk needs a free accumulator: with none, the idle lanes wait
                     // for one of the wave's open chunks to finish (every open chunk
                     // has a sample in flight, so one will).
-                    if (!join && acc_free == 0ull) {
+                    if (acc_free == 0ull) {
                         // Retire the chunks no busy lane traces any more (lanes assigned in
                         // this refill have not started yet: their chunk is open regardless).
                         const bool held = L.busy || fresh_item != ~0u;
                         acc_free = acc_retire(p, acc, acc_all, held, L.busy ? L.slot : fresh_slot, acc_chunk, lane);
                     }
-                    if (!join && acc_free == 0ull) {
+                    if (acc_free == 0ull) {
                         // unreachable with nothing in flight: no chunk would hold a slot
                         if (__ballot(L.busy || fresh_item != ~0u) == 0ull) __builtin_trap();
                         break;
@@ -1332,13 +1319,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     int32_t cx, cj;
                     uint32_t cs, cp;
                     if (pool_next < p.items && decode_item(p, pool_next, cx, cj, cs, cp)) {
-                        if (join) {  // one more chunk in the current slot's run
-                            acc_chunk = lane == pool_slot ? acc_chunk + (1u << kAccRunShift) : acc_chunk;
-                        } else {
-                            pool_slot = (uint32_t)__builtin_ctzll(acc_free);
-                            acc_free &= ~(1ull << pool_slot);
-                            acc_chunk = lane == pool_slot ? c | (1u << kAccRunShift) : acc_chunk;
-                        }
+                        pool_slot = (uint32_t)__builtin_ctzll(acc_free);
+                        acc_free &= ~(1ull << pool_slot);
+                        acc_chunk = lane == pool_slot ? c : acc_chunk;
                     }
                 }
             }
@@ -1711,13 +1694,9 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
         const AccPartial* part = reinterpret_cast<const AccPartial*>(p.samples) + (item0 >> 6);
         int64_t s[3] = {0, 0, 0};
         uint32_t bad = 0u;
-        // the pixel-pass's accumulator runs, each recorded at its first chunk
-        for (int32_t c = 0; c < p.spp / 64;) {
-            const AccPartial r = part[c];
+        for (int32_t c = 0; c < p.spp / 64; ++c)
 #pragma unroll
-            for (int k = 0; k < 3; ++k) acc_add(r.sum[k], 0x1p53, s[k], bad, k);
-            c += max((int32_t)r.chunks, 1);
-        }
+            for (int k = 0; k < 3; ++k) acc_add(part[c].sum[k], 0x1p53, s[k], bad, k);
         write_acc_mean<kFmt>(p, srgb, s, bad, x, j, pass);
         return;
     } else if constexpr (kMode == kResolveFixed) {

@@ -105,8 +105,7 @@ struct KernelParams {
     // the background is pre-scaled by 2^acc_shift, each sample's scaled colour is rounded to
     // an integer and the integers are summed exactly (order-free); 0: FP64 sum in sample order.
     int32_t acc_shift;
-    int32_t acc_slots;   // >0: per-wave LDS accumulators (slots per wave), partial per run of 64-item chunks
-    uint32_t acc_run_max;  // consecutive chunks of one pixel-pass one accumulator may hold (fixed_point, tray_abi.hip)
+    int32_t acc_slots;   // >0: per-wave LDS accumulators (slots per wave), partial per 64-item chunk
     uint32_t acc_off;    // byte offset of the accumulator region in the kernel's dynamic LDS
     const Bvh4Node* nodes;  // exact-culling 4-wide BVH (tray_bvh.cpp), root first
     const int32_t* leaves;  // per leaf: (first slot << 3) | count
@@ -153,24 +152,11 @@ constexpr int32_t kAccBits = 47;
 // A frame whose colour bound leaves the scale 2^k below 2^kAccMinShift (the
 // absolute resolution of a sample, 2^-k) keeps the FP64 sum in sample order.
 constexpr int32_t kAccMinShift = 44;
-// One accumulator run's sums in global memory (exact integers held as doubles):
-// 32 B, at the record index of the run's first chunk; `chunks` is the run's
-// length (consecutive chunks of one pixel-pass, 1..kAccRunMax). The records of
-// a run's other chunks are never written nor read: the resolve pass walks a
-// pixel-pass's runs from its first chunk.
+// One chunk's sums in global memory (exact integers held as doubles): 32 B.
 struct AccPartial {
     double sum[3];
-    double chunks;
+    double pad;
 };
-// Runs of up to 2^kAccRunLog2Max chunks (r >= 128: one record per 256 samples
-// instead of per 64); a run's sum stays exact because its samples use
-// kAccBits - log2(run) bits (fixed_point, tray_abi.hip).
-constexpr int32_t kAccRunLog2Max = 2;
-constexpr uint32_t kAccRunMax = 1u << kAccRunLog2Max;
-// The kernel keeps a slot's (first chunk, run length) in one word: chunk indices
-// of a band are < 2^25 (items < 2^31).
-constexpr uint32_t kAccRunShift = 26;
-constexpr uint32_t kAccChunkMask = (1u << kAccRunShift) - 1u;
 static_assert(sizeof(AccPartial) == 32, "AccPartial layout");
 // In LDS each open chunk has TRAY_ACC_COPIES sets of three sums; lane l adds to
 // set l % copies, so fewer lanes of a wave hit one address in one instruction.
