@@ -120,7 +120,17 @@ static void trace(const Bvh& b, const Seg& s, Count& c, int* hit_index) {
                 memcpy(&u, &tn, 4);
                 key[k] = tn <= tf ? ((u & 0xFFFF0000u) | nd.ref[k]) : ~0u;
             }
-            std::sort(key, key + 4);
+            static const int order_mode = getenv("BVH_SIM_ORDER") ? atoi(getenv("BVH_SIM_ORDER")) : 0;
+            if (order_mode == 0) {
+                std::sort(key, key + 4);  // the kernel: full sort, nearest visited, the rest pushed far-to-near
+            } else {  // 1: nearest first, the rest in child order (hit keys before misses)
+                int m = 0;
+                for (int k = 1; k < 4; ++k)
+                    if (key[k] < key[m]) m = k;
+                std::swap(key[0], key[m]);
+                std::stable_partition(key + 1, key + 4, [](uint32_t x) { return x != ~0u; });
+                if (order_mode == 2) std::reverse(key + 1, key + 1 + (int)std::count_if(key + 1, key + 4, [](uint32_t x) { return x != ~0u; }));
+            }
             if (key[0] != ~0u) {
                 for (int k = 3; k >= 1; --k)
                     if (key[k] != ~0u) {

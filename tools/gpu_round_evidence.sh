@@ -16,7 +16,7 @@ timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $O/bench_c2.log 2>&1 
 bash tools/gpu_profile_all.sh $O/all || exit 1
 # the other configs in the headline launch shape (the driver's --steps 20 --warmup 5: 16-frame launches)
 for c in c1 c3 c5; do
-  timeout -k 10 300 python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_$c.log 2>&1 || exit 1
+  timeout -k 10 400 python3 bench.py --config $c --steps 20 --warmup 5 > $O/bench_$c.log 2>&1 || exit 1
 done
 timeout -k 10 300 python3 tools/shard_sim.py --ns 1,2,4,8 --passes 16 --frames-in-flight 2 --reps 24 > $O/shard_c2.jsonl 2>&1 || exit 1
 echo ok > $O/done
