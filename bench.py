@@ -26,8 +26,9 @@ line and every point of a 1 -> 8 curve share one launch shape) renders F
 frames per launch (tray_render_passes_async: lanes flow from one frame's
 samples into the next, so a launch has one tail of long paths, not F); at
 N > 1 one gather per launch moves its F frames to rank 0, on a stream of its
-own. Launches rotate over --frames-in-flight slots (own device scene - work
-queue, sample buffer -, output and stream; default 2), so a launch's
+own. Launches rotate over --frames-in-flight slots (own output and stream, and
+the one device scene's launch context of that stream - work queue, chunk
+records -; default 2), so a launch's
 workgroups start on the CUs the previous launch's last long paths leave idle.
 Every step still renders its whole frame inside the timed region.
 
@@ -287,14 +288,17 @@ def main() -> int:
     # A step is one frame. Frames are rendered F per launch at every N (progressive
     # passes of tray_render_passes_async: lanes flow from one frame's samples into
     # the next, so a launch has one tail of long paths, not F), and launches
-    # rotate over frame slots (own device scene - work queue and sample buffer -,
-    # output and stream), so launch j+1 starts on the CUs launch j's last paths
-    # leave idle. At N > 1 each launch's F frames are gathered to rank 0 with ONE
+    # rotate over frame slots (own output and stream; the scene's launch context of
+    # that stream holds the work queue and chunk records), so launch j+1 starts on
+    # the CUs launch j's last paths leave idle. At N > 1 each launch's F frames are gathered to rank 0 with ONE
     # gather on a stream of its own; the next launch into the same slot waits for it.
     F = max(1, min(args.passes, args.steps))
     nslot = max(1, args.frames_in_flight)
-    scenes = [_lib.DeviceScene(spheres, bg, local_rank) for _ in range(nslot)]
-    plan = scenes[0].plan(cam._state, params, F).as_dict()  # tray_render_plan_get: how the timed launches run
+    # ONE device scene for every slot: each slot's stream gets a launch context of its own
+    # (work queue, chunk records, candidate records; include/tray.h "Concurrency"), so the
+    # launches in flight share the scene as goroutines share a *Scene.
+    scene = _lib.DeviceScene(spheres, bg, local_rank)
+    plan = scene.plan(cam._state, params, F).as_dict()  # tray_render_plan_get: how the timed launches run
     outs = [torch.empty((F, rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nslot)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nslot - 1)]
     comm = torch.cuda.Stream() if world > 1 else None
@@ -306,16 +310,16 @@ def main() -> int:
             gathers[(k, n)] = shard.FrameGather(n, H, W, (3,), args.tile_rows, world, rank, torch.float32,
                                                 torch.device("cuda", local_rank))
         return gathers[(k, n)]
-    scene, out, stream = scenes[0], outs[0], streams[0]
+    out, stream = outs[0], streams[0]
 
     def launch(k, first, n):
         """Frames first .. first + n - 1 (progressive passes) in slot k."""
         p = _lib.Params.from_buffer_copy(params)
         p.pass_ = first % 4096
         if n == 1:
-            scenes[k].render_async(cam._state, p, outs[k].data_ptr(), None, streams[k].cuda_stream)
+            scene.render_async(cam._state, p, outs[k].data_ptr(), None, streams[k].cuda_stream)
         else:
-            scenes[k].render_passes_async(cam._state, p, n, outs[k].data_ptr(), streams[k].cuda_stream)
+            scene.render_passes_async(cam._state, p, n, outs[k].data_ptr(), streams[k].cuda_stream)
 
     def frames(first, count):
         j = 0
@@ -537,8 +541,7 @@ def main() -> int:
                                          else "--no-cpu-baseline: no oracle frame")
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    for sc in scenes:
-        sc.release()
+    scene.release()
     if dist:
         dist.destroy_process_group()
     return 0

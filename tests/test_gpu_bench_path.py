@@ -1,16 +1,16 @@
 """The exact path bench.py times, checked against the oracle at its own size.
 
-bench.py (`launch`/`frames`, bench.py:275-299) renders F = 16 progressive
-passes per launch through tray_render_passes_async into TRAY_OUT_RGB_F32, with
-two frame slots (own DeviceScene - work queue, chunk records -, output and
-stream) in flight at once, and with 64 | r every pixel's samples summed on chip
+bench.py (`launch`/`frames`) renders F = 16 progressive passes per launch
+through tray_render_passes_async into TRAY_OUT_RGB_F32, with two frame slots
+(own output and stream, ONE DeviceScene whose launch context per stream holds
+the work queue and chunk records) in flight at once, and with 64 | r every pixel's samples summed on chip
 as exact fixed-point chunk sums ("Accumulation"). This test runs
 that shape for C2 (the headline) and C5 (dense scene: LDS layout 2, four
 64-sample chunks per pixel):
 
   launch A: slot 0, passes  0..15     (in flight together with B)
   launch B: slot 1, passes 16..31
-  launch C: slot 0, passes 32..47     (the same scene again: its work queue
+  launch C: slot 0, passes 32..47     (slot 0's context again: its work queue
                                        must have been re-zeroed by A's resolve)
 
 and checks frames 0, 7, 15 of A, 0 and 15 of B and 15 of C (passes 0, 7, 15,
@@ -63,9 +63,9 @@ def test_bench_launch_shape_vs_oracle(L, O, config):
     cam.Initialize(W, H)
     bg = ray._background(ray.DefaultBackground())
     params = L.make_params(W, H, depth, spp, 0.5, seed, output=L.OUT_RGB_F32)
-    scenes = [L.DeviceScene(spheres, bg, 0) for _ in range(2)]
+    scene = L.DeviceScene(spheres, bg, 0)  # one scene, two streams (bench.py)
     try:
-        plan = scenes[0].plan(cam._state, params, F).as_dict()
+        plan = scene.plan(cam._state, params, F).as_dict()
         assert plan["acc_slots"] > 0 and plan["fixed_point_shift"] > 0, plan  # the on-chip sums bench.py times
         if config == "c5":
             assert plan["lds_layout"] == 2, plan
@@ -75,7 +75,7 @@ def test_bench_launch_shape_vs_oracle(L, O, config):
             p = L.Params.from_buffer_copy(params)
             p.pass_ = first
             with torch.cuda.stream(streams[slot]):
-                scenes[slot].render_passes_async(cam._state, p, F, outs[name].data_ptr(), streams[slot].cuda_stream)
+                scene.render_passes_async(cam._state, p, F, outs[name].data_ptr(), streams[slot].cuda_stream)
         torch.cuda.synchronize()
         rng = np.random.default_rng({"c2": 42, "c5": 57}[config])
         single = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
@@ -87,7 +87,7 @@ def test_bench_launch_shape_vs_oracle(L, O, config):
                 bench_frame = outs[name][f]
                 p = L.Params.from_buffer_copy(params)
                 p.pass_ = k
-                scenes[0].render_async(cam._state, p, single.data_ptr(), seg.data_ptr(), stream)
+                scene.render_async(cam._state, p, single.data_ptr(), seg.data_ptr(), stream)
                 torch.cuda.synchronize()
                 assert torch.equal(bench_frame, single), f"{config} pass {k}: passes launch != single render"
                 got = bench_frame.cpu().numpy()
@@ -106,5 +106,4 @@ def test_bench_launch_shape_vs_oracle(L, O, config):
                 assert np.all(np.abs(g - ref) <= tol), f"{config} pass {k}: {float(np.abs(g - ref).max())}"
                 assert (got[ys, xs] == ref.astype(np.float32)).mean() >= 0.999
     finally:
-        for s in scenes:
-            s.release()
+        scene.release()
