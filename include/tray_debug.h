@@ -29,6 +29,9 @@
  *   "scene_contexts"      launch contexts per scene (default 4): renders of one
  *                         scene beyond this many in flight wait for the least
  *                         recently used one; 1 serialises them (same bits)
+ *   "grid_reserve"        workgroup slots the persistent render grid leaves
+ *                         free on the device (0..CUs-1), for kernels that run
+ *                         beside it: collectives, copies (same bits)
  */
 #ifndef TRAY_DEBUG_H
 #define TRAY_DEBUG_H

@@ -39,7 +39,7 @@ static std::atomic<long long> g_knob_value[kKnobCount];
 static std::atomic<bool> g_knob_set[kKnobCount];
 static const char* const kKnobNames[kKnobCount] = {
     "acc_slots", "band_samples", "bvh_leaf", "bvh_lds_mode", "stack_lds_slots", "node_deep", "primary_candidates",
-    "resolve_staged", "wave_chunks", "scene_contexts"};
+    "resolve_staged", "wave_chunks", "scene_contexts", "grid_reserve"};
 
 bool debug_knob(DebugKnob k, long long* v) {
     if (!g_knob_set[k].load(std::memory_order_acquire)) return false;

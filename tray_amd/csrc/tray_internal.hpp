@@ -34,6 +34,7 @@ enum DebugKnob {
     kKnobResolveStaged,
     kKnobWaveChunks,
     kKnobSceneContexts,
+    kKnobGridReserve,
     kKnobCount
 };
 // True, with the value in *v, when the knob is set.

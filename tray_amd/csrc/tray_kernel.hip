@@ -2181,6 +2181,9 @@ hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, h
         e = hipMemsetAsync(p.segments, 0, (size_t)p.rows * (size_t)p.width * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
+    long long reserve_knob = 0;
+    (void)debug_knob(kKnobGridReserve, &reserve_knob);
+    const int reserve = (int)std::min<long long>(std::max<long long>(reserve_knob, 0), blocks - 1);
     long long wave_chunks_knob = 0;
     (void)debug_knob(kKnobWaveChunks, &wave_chunks_knob);
     wave_chunks_knob = std::min<long long>(std::max<long long>(wave_chunks_knob, 0), 64);
@@ -2204,8 +2207,9 @@ hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, h
             p.wave_chunks = (uint32_t)wave_chunks_knob;
             p.late_at = p.nchunks;
         }
-        // Enough waves for every chunk, capped at what the device keeps resident.
-        const uint32_t grid = std::min<uint32_t>((p.nchunks + waves - 1u) / waves, (uint32_t)blocks);
+        // Enough waves for every chunk, capped at what the device keeps resident
+        // (less the slots the "grid_reserve" knob leaves to other kernels).
+        const uint32_t grid = std::min<uint32_t>((p.nchunks + waves - 1u) / waves, (uint32_t)(blocks - reserve));
         // The queue is zero here: zeroed at allocation and by every resolve pass.
         hipLaunchKernelGGL(fn, dim3(grid), dim3(threads), lds, stream, p);
         e = hipGetLastError();
