@@ -189,6 +189,29 @@ def launch_ranks(n: int, argv: list, timeout: float | None = None, script: str |
     return rc
 
 
+_PHASE = ["start"]
+
+
+def set_phase(name: str) -> None:
+    """What this rank is doing, for the watchdog's message."""
+    _PHASE[0] = name
+
+
+def start_watchdog(rank: int, seconds: float) -> None:
+    """A daemon thread that ends this rank (exit status 124) once it has run for
+    `seconds`, naming the rank and its phase: a collective that never completes
+    (a peer that died, an RCCL hang) then fails the job instead of holding it."""
+    import threading
+
+    def watch():
+        time.sleep(seconds)
+        print(f"bench.py: rank {rank} still running after {seconds} s (--rank-timeout), in phase "
+              f"'{_PHASE[0]}': exiting", file=sys.stderr, flush=True)
+        os._exit(124)
+
+    threading.Thread(target=watch, daemon=True, name="rank-watchdog").start()
+
+
 def device_record(torch, local_rank: int) -> dict:
     """Which device this rank renders on (bench line, `dist.devices`)."""
     pr = torch.cuda.get_device_properties(local_rank)
@@ -220,8 +243,9 @@ def main() -> int:
                     help="frames per launch, the same at every N (tray_render_passes_async: consecutive "
                          "progressive passes in one persistent launch, one tail of long paths per launch)")
     ap.add_argument("--rank-timeout", type=float, default=900.0,
-                    help="self-launched ranks (--gpus N > 1 without a launcher): stop them after this many seconds "
-                         "and exit non-zero, naming the ranks still running (0: no limit)")
+                    help="N > 1: a rank still running after this many seconds exits 124 naming its phase (under any "
+                         "launcher; also the process group's collective timeout), and bench.py's own launcher stops "
+                         "the ranks still running (0: no limit)")
     ap.add_argument("--cpu-min-seconds", type=float, default=10.0,
                     help="cpu_baseline: render further progressive passes of the sample until this much time has "
                          "passed (small frames, C1)")
@@ -232,10 +256,15 @@ def main() -> int:
         # No launcher: start the N ranks here, before anything touches the GPU.
         return launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout if args.rank_timeout > 0 else None)
 
-    import torch
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world > 1 and args.rank_timeout > 0:
+        # Under any launcher (torchrun included) a rank stuck in a collective ends with a
+        # non-zero exit that names it and the phase it was in, instead of hanging.
+        start_watchdog(rank, args.rank_timeout)
+
+    import torch
+
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # TRAY_BENCH_BACKEND=gloo rehearses the N > 1 code path on ONE GPU (ranks
     # share device 0; RCCL refuses two ranks on one device). Never for numbers.
@@ -260,10 +289,14 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist
 
+        from datetime import timedelta
+
+        set_phase("init_process_group")
+        to = {"timeout": timedelta(seconds=args.rank_timeout)} if args.rank_timeout > 0 else {}
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), **to)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **to)
         # What the process group saw: its size and every rank's device.
         devs = [None] * world
         dist.all_gather_object(devs, dict(device_record(torch, local_rank), rank=rank))
@@ -276,6 +309,7 @@ def main() -> int:
 
     from tray_amd import _lib, ray, shard
 
+    set_phase("scene upload")
     label, seed, half, W, H, spp, depth = CONFIGS[args.config]
     spheres = ray.rich_scene_array(seed, half)
     cam = ray.RichSceneCamera()
@@ -355,10 +389,12 @@ def main() -> int:
         if world > 1:  # and its gather buffers, for every launch size the timed frames use
             for n in {F, args.steps % F} - {0}:
                 gather_for(k, n)
+    set_phase("warmup")
     frames(0, args.warmup)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    set_phase("timed frames")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     frames(args.warmup, args.steps)
@@ -378,6 +414,7 @@ def main() -> int:
         torch.cuda.synchronize()
         return float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
+    set_phase("launch timings")
     kernel_ms = launch_ms(F)  # the timed launch shape: F frames, megakernel + F resolves
     single_ms = kernel_ms if F == 1 else None if args.no_single else launch_ms(1)  # one frame, nothing overlapped
     ranks_rec = None
@@ -385,6 +422,7 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        set_phase("per-rank gather timing")
         # Untimed, per rank: the render of its rows (kernel_ms above) and one gather of F frames
         # (HIP events on the gather's stream), so a measured curve separates imbalance from the gather.
         torch.cuda.synchronize()
@@ -541,6 +579,7 @@ def main() -> int:
                                          else "--no-cpu-baseline: no oracle frame")
     if rank == 0:
         print(json.dumps(rec), flush=True)
+    set_phase("teardown")
     scene.release()
     if dist:
         dist.destroy_process_group()

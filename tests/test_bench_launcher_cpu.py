@@ -166,3 +166,17 @@ def test_frame_parity_record():
     seg2[0, 0] += 1
     rec = bench.frame_parity(ref, seg, bad, seg2, ref.astype(np.float32))
     assert not rec["ok"] and abs(rec["linf"] - 2e-4) < 1e-12 and rec["segments_differing"] == 1
+
+
+def test_rank_watchdog_names_rank_and_phase():
+    """Under any launcher (torchrun included) an N > 1 rank that is still running
+    after --rank-timeout exits 124 and names itself and its phase (bench.py
+    start_watchdog), so a collective that never completes fails the job."""
+    import time
+
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; bench.start_watchdog(3, 1.0); "
+            "bench.set_phase('timed frames'); time.sleep(60)" % ROOT)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 124 and time.monotonic() - t0 < 30
+    assert "rank 3 still running after 1.0 s" in r.stderr and "'timed frames'" in r.stderr
