@@ -703,9 +703,29 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     LaunchCtx* c = nullptr;
     rc = take_ctx(sc, stream, &c);
     if (rc) return rc;
-    TRAY_HIP(grow_ctx_buffer(c, reinterpret_cast<void**>(&c->samples), &c->samples_bytes, plan.buffer_bytes));
-    if (use_bvh && k.stack_cap > plan.layout.stack_lds)
-        TRAY_HIP(grow_ctx_buffer(c, reinterpret_cast<void**>(&c->stack_ovf), &c->ovf_bytes, sc->ovf_bytes));
+    // From here on something may be enqueued on `stream` that uses the context
+    // (its queue zeroing, a candidate build, a band): every exit records the
+    // context's event after it, so the next user waits for it.
+    auto finish = [&](hipError_t e, const char* what) -> int {
+        const hipError_t r = hipEventRecord(c->done, stream);
+        c->launched = c->launched || r == hipSuccess;
+        c->last_stream = stream;
+        c->last_use = ++sc->launches;
+        if (e == hipSuccess && r != hipSuccess) {  // nothing marks the render's end: wait for it here
+            (void)hipStreamSynchronize(stream);
+            e = r;
+            what = "hipEventRecord";
+        }
+        if (e != hipSuccess) {
+            if (r != hipSuccess) (void)hipStreamSynchronize(stream);
+            return hip_fail(e, what);
+        }
+        return TRAY_OK;
+    };
+    hipError_t e = grow_ctx_buffer(c, reinterpret_cast<void**>(&c->samples), &c->samples_bytes, plan.buffer_bytes);
+    if (e == hipSuccess && use_bvh && k.stack_cap > plan.layout.stack_lds)
+        e = grow_ctx_buffer(c, reinterpret_cast<void**>(&c->stack_ovf), &c->ovf_bytes, sc->ovf_bytes);
+    if (e != hipSuccess) return finish(e, "launch context buffers");
     k.queue = c->queue;
     k.samples = c->samples;
     k.stack_ovf = c->stack_ovf;
@@ -719,26 +739,16 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         key.multi_sample = p->rays_per_pixel > 1;
         if (!c->cand_valid || memcmp(&key, &c->cand_key, sizeof(key)) != 0) {
             c->cand_valid = false;
-            TRAY_HIP(grow_ctx_buffer(c, reinterpret_cast<void**>(&c->cand), &c->cand_bytes,
-                                     cand_workspace_bytes(p->width, k.rows)));
-            TRAY_HIP(launch_cand_build(k, c->cand, stream));
+            e = grow_ctx_buffer(c, reinterpret_cast<void**>(&c->cand), &c->cand_bytes,
+                                cand_workspace_bytes(p->width, k.rows));
+            if (e == hipSuccess) e = launch_cand_build(k, c->cand, stream);
+            if (e != hipSuccess) return finish(e, "candidate lists");
             c->cand_key = key;
             c->cand_valid = true;
         }
         k.cand = c->cand;
     }
-    const hipError_t e = launch_render(k, use_bvh, plan, stream, c->samples_bytes);
-    // Recorded even after a failure: a band may already be enqueued.
-    const hipError_t r = hipEventRecord(c->done, stream);
-    c->launched = c->launched || r == hipSuccess;
-    c->last_stream = stream;
-    c->last_use = ++sc->launches;
-    if (e != hipSuccess) return hip_fail(e, "launch_render");
-    if (r != hipSuccess) {  // nothing marks the render's end: wait for it here
-        (void)hipStreamSynchronize(stream);
-        return hip_fail(r, "hipEventRecord");
-    }
-    return TRAY_OK;
+    return finish(launch_render(k, use_bvh, plan, stream, c->samples_bytes), "launch_render");
 }
 
 int tray_render_plan_get(tray_scene_t sc, const tray_camera* cam, const tray_params* p, int32_t n_passes,
