@@ -159,16 +159,15 @@ typedef struct tray_params {
  * results; the flag exists for verification and A/B timing. */
 #define TRAY_FLAG_LINEAR_SCAN 1
 
-/* Pixel sums. DEFAULT (flag clear): when rays_per_pixel is a multiple of 64 and
- * the scene's colour bound allows it, each pixel's samples are summed exactly
+/* Pixel sums. DEFAULT (flag clear): when rays_per_pixel is a multiple of 64, or
+ * 16 or 32, and the scene's colour bound allows it, each pixel's samples are summed exactly
  * as fixed-point integers of 2^-k (k >= 44), so the mean is within 2^-(k+1) of
  * the exact mean of the sample colours and does not depend on the order in
  * which samples finish (tray_render_plan_get reports k; C2: k = 46, L-inf
  * 6.7e-15 against the sequential FP64 sum). With TRAY_FLAG_ORDERED_SUM the
  * samples are added in sample order in FP64, exactly as Go's RenderLines
  * accumulates colorSum (ray/tracer.go:143), at the cost of a 24-B per-sample
- * device buffer. Renders whose r is not a multiple of 64 always use the
- * ordered sum. Both are far inside the 1e-4 parity gate; the flag selects the
+ * device buffer. Renders with any other r always use the ordered sum. Both are far inside the 1e-4 parity gate; the flag selects the
  * bits. */
 #define TRAY_FLAG_ORDERED_SUM 2
 
@@ -302,13 +301,14 @@ int tray_scene_get_info(tray_scene_t scene, tray_scene_info *out);
 
 /* How a render of `params` (n_passes progressive passes from params->pass) on
  * `scene` with `camera` would run, without running it. Pixel sums: with
- * fixed_point_shift k > 0 (rays_per_pixel a multiple of 64 and a colour bound
+ * fixed_point_shift k > 0 (rays_per_pixel a multiple of 64, or 16 or 32, and a colour bound
  * that allows k >= 44) each pixel's samples are summed exactly as integers of
  * 2^-k, so the mean is within 2^-(k+1) of the exact mean of the sample colours
  * whatever order the samples finish in; k = 0: the FP64 sum in sample order of
  * Go's RenderLines (ray/tracer.go:143). acc_slots > 0: those sums are kept on
- * chip (per-wave LDS accumulators, one 32-B record per 64 samples in
- * buffer_bytes); 0: through a 24-B per-sample buffer. Both give the same bits. */
+ * chip (per-wave LDS accumulators, one 32-B record per 64 samples, or per
+ * pixel-pass when r is 16 or 32, in buffer_bytes); 0: through a 24-B
+ * per-sample buffer. Both give the same bits. */
 typedef struct tray_render_plan {
     int32_t fixed_point_shift; /* k (0: FP64 sum in sample order) */
     int32_t acc_slots;         /* on-chip accumulators per wave (0: per-sample buffer) */

@@ -1,10 +1,11 @@
 """Fixed-point accumulation of a pixel's samples ("Accumulation").
 
-Frames whose rays_per_pixel is a multiple of 64 (every benchmark config but C1)
-sum each pixel's samples exactly as integers (the colour scaled by 2^k and
-rounded, k >= 44, so the mean is within 2^-45 of the exact mean of the FP64
-sample colours), on chip per 64-sample chunk when the LDS has room, else
-through the per-sample buffer. Both mechanisms give the same bits, whatever the
+Frames whose rays_per_pixel is a multiple of 64, or 16 or 32 (every benchmark
+config) sum each pixel's samples exactly as integers (the colour scaled by 2^k
+and rounded, k >= 44, so the mean is within 2^-45 of the exact mean of the FP64
+sample colours), on chip when the LDS has room (per 64-sample chunk, or per
+pixel-pass of a chunk that holds 64 / r of them), else through the per-sample
+buffer. Both mechanisms give the same bits, whatever the
 order the samples finish in; against the oracle (Go's FP64 sum in sample order)
 the frames stay inside the parity bar of tests/test_gpu_parity.py (paths
 bit-exact, colour within 1e-12). Other frames keep the FP64 sum in sample order.
@@ -24,7 +25,9 @@ FIXED_TOL = 2.0 ** -44  # fixed point vs the FP64 sum of the same samples: 2^-45
 
 
 # width/height not multiples of 8: padding pixels in the last tiles (chunks that start no sample)
-@pytest.mark.parametrize("scene,spp", [("rich2", 64), ("rich2", 128), ("dense7", 64), ("rich2", 256), ("dense7", 192)])
+# r = 16 / 32: a chunk is 4 / 2 pixel-passes (here pixels: one pass), padding and real pixels mixed
+@pytest.mark.parametrize("scene,spp", [("rich2", 64), ("rich2", 128), ("dense7", 64), ("rich2", 256), ("dense7", 192),
+                                       ("rich2", 16), ("rich2", 32), ("dense7", 16)])
 def test_on_chip_equals_sample_buffer_and_oracle(L, O, scene, spp):
     sc = O.rich_scene(2) if scene == "rich2" else O.rich_scene(7, 22)
     w, h = 37, 21
@@ -40,29 +43,31 @@ def test_on_chip_equals_sample_buffer_and_oracle(L, O, scene, spp):
     check(base, bseg, ref, rseg)
 
 
-def test_fixed_point_vs_fp64_sum(L, O):
+@pytest.mark.parametrize("spp", [64, 16])
+def test_fixed_point_vs_fp64_sum(L, O, spp):
     sc = O.rich_scene(2)
     w, h = 48, 27
     st = camera(L, RICH_SETUP, w, h)
-    fixed, fseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 6)
-    f64, dseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 6, flags=L.FLAG_ORDERED_SUM)
+    fixed, fseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 6)
+    f64, dseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 6, flags=L.FLAG_ORDERED_SUM)
     assert np.array_equal(fseg, dseg)
     err = float(np.max(np.abs(fixed - f64)))
     assert err <= FIXED_TOL, err
     assert not np.array_equal(fixed, f64)  # the two sums do differ in the last bits somewhere
 
 
-def test_fixed_point_formats_and_linear_scan(L, O):
+@pytest.mark.parametrize("spp", [64, 32])
+def test_fixed_point_formats_and_linear_scan(L, O, spp):
     sc = O.rich_scene(2)
     w, h = 40, 22
     st = camera(L, RICH_SETUP, w, h)
-    f64, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3)
-    f32, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3, output=L.OUT_RGB_F32)
+    f64, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 3)
+    f32, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 3, output=L.OUT_RGB_F32)
     assert np.array_equal(f32, f64.astype(np.float32))
-    u8, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3, output=L.OUT_RGBA8)
+    u8, _ = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 3, output=L.OUT_RGBA8)
     assert np.array_equal(u8, O.to_srgba(f64))
     # the linear-scan kernel sums through the per-sample buffer: same bits
-    lin, lseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, 64, 50, 0.5, 3, flags=L.FLAG_LINEAR_SCAN)
+    lin, lseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 3, flags=L.FLAG_LINEAR_SCAN)
     assert np.array_equal(lseg, seg) and np.array_equal(lin, f64)
 
 
@@ -82,7 +87,10 @@ def test_bound_too_large_keeps_fp64_sum(L, O):
     assert float(np.max(np.abs(a - ref))) <= 1e-12 * max(1.0, float(np.max(np.abs(ref))))
 
 
-def test_passes_and_tiles_with_chunk_partials(L, O):
+# r = 16 with 3 and 4 passes per launch: a chunk's four pixel-passes straddle pixels
+# (3) or are one pixel's passes (4)
+@pytest.mark.parametrize("spp,passes", [(128, 3), (16, 3), (16, 4), (32, 5)])
+def test_passes_and_tiles_with_chunk_partials(L, O, spp, passes):
     """Several progressive passes in one launch (partials of every pass in one
     buffer), row tiles, and a short launch band: bit-identical to single renders."""
     import torch
@@ -90,17 +98,18 @@ def test_passes_and_tiles_with_chunk_partials(L, O):
     from test_gpu_parity import _passes
 
     sc = O.rich_scene(2)
-    w, h, spp = 40, 19, 128
+    w, h = 37, 19
     st = camera(L, RICH_SETUP, w, h)
     dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
     try:
-        for band in (None, 40 * 8 * spp * 3 * 2):
+        assert dev.plan(st, L.make_params(w, h, 50, spp, 0.5, 4), passes).acc_slots > 0
+        for band in (None, 40 * 8 * spp * passes * 2):
             with L.debug_knobs(band_samples=band):
                 for tiles in [{}, dict(tile_rows=2, tile_count=3, tile_index=1)]:
                     p = L.make_params(w, h, 50, spp, 0.5, 4, pass_=1, **tiles)
                     rows = L.params_rows(p)
-                    frames = _passes(L, dev, st, p, 3, torch.float64, (rows, w, 3))
-                    for k in range(3):
+                    frames = _passes(L, dev, st, p, passes, torch.float64, (rows, w, 3))
+                    for k in range(passes):
                         q = L.make_params(w, h, 50, spp, 0.5, 4, pass_=1 + k, **tiles)
                         one, _ = L.render(sc, bg_struct(L, DEFAULT_BG), st, q, 0)
                         assert np.array_equal(frames[k], one), (band, tiles, k)
@@ -109,8 +118,9 @@ def test_passes_and_tiles_with_chunk_partials(L, O):
 
 
 def test_render_plan(L, O):
-    """tray_render_plan_get reports which accumulation a render runs: the benchmark
-    configs C2-C5 sum on chip, C1 (r = 16) keeps the FP64 sum in sample order."""
+    """tray_render_plan_get reports which accumulation a render runs: every benchmark
+    config sums on chip, C1 (r = 16) one record per pixel-pass, the others one per
+    64 samples; r = 8 keeps the FP64 sum in sample order."""
     from bench import CONFIGS
     from tray_amd import ray
 
@@ -132,13 +142,23 @@ def test_render_plan(L, O):
             assert dev.plan(cam._state, lin, 1).bvh == 0 and dev.plan(cam._state, lin, 1).acc_slots == 0
         finally:
             dev.release()
-    assert plans["c1"]["fixed_point_shift"] == 0 and plans["c1"]["acc_slots"] == 0
-    for c in ("c2", "c5"):
+    for c in ("c1", "c2", "c5"):
         assert plans[c]["fixed_point_shift"] == 46 and plans[c]["acc_slots"] >= 8 and plans[c]["bvh"] == 1, plans[c]
     assert plans["c2"]["lds_layout"] == 1 and plans["c5"]["lds_layout"] == 2
     # C2, 16 frames: one band, one 32-B record per 64 samples
     assert plans["c2"]["buffer_bytes"] == 1280 * 720 * 64 * 16 // 64 * 32
     assert plans["c2"]["lds_bytes"] <= 160 * 1024
+    # C1, 16 frames: one band, one 32-B record per pixel-pass (r = 16), padded to 8x8 tiles
+    assert plans["c1"]["buffer_bytes"] == 50 * 29 * 64 * 16 * 32 and plans["c1"]["lds_bytes"] <= 160 * 1024
+    _, seed, half, w, h, _, depth = CONFIGS["c1"]
+    cam = ray.RichSceneCamera()
+    cam.Initialize(w, h)
+    dev = L.DeviceScene(ray.rich_scene_array(seed, half), ray._background(ray.DefaultBackground()), 0)
+    try:
+        p8 = dev.plan(cam._state, L.make_params(w, h, depth, 8, 0.5, seed), 16)
+        assert p8.fixed_point_shift == 0 and p8.acc_slots == 0
+    finally:
+        dev.release()
 
 
 def test_ordered_sum_flag_vs_oracle(L, O):

@@ -38,7 +38,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tray_amd", "csrc", "tray_kernel.hip")
-KERNEL = "_ZN4tray13render_kernelILi1ELb1ELb0ELb0ELb0ELb1ELi5EEEvNS_12KernelParamsE"  # --layout 2: ...ILi2E...
+KERNEL = "_ZN4tray13render_kernelILi1ELb1ELb0ELb0ELb0ELi1ELi5EEEvNS_12KernelParamsE"  # --layout 2: ...ILi2E...
 LLVM = "/opt/rocm/lib/llvm/bin"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", "-mllvm",
          "-amdgpu-atomic-optimizer-strategy=None"]

@@ -18,20 +18,21 @@ def main():
     ap.add_argument("root", help="gpu_profile_all.sh output dir (holds pmc1/, pmc2/)")
     ap.add_argument("--label", default="")
     ap.add_argument("--frames", type=int, default=16, help="frames per launch of the profiled bench command")
-    ap.add_argument("--config", default="c2", help="bench config: picks the kernel instance (on-chip sums iff 64 | r)")
+    ap.add_argument("--config", default="c2", help="bench config: picks the kernel instance (how r is summed)")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import CONFIGS
 
-    acc = CONFIGS[a.config][5] % 64 == 0
-    want = ", true, false, false, false, true, " if acc else ", true, false, false, false, false, "
+    spp = CONFIGS[a.config][5]
+    # kAcc: 1 on-chip sums per 64-sample chunk (64 | r), 2 per pixel-pass (r = 16, 32), 0 none
+    want = f", true, false, false, false, {1 if spp % 64 == 0 else 2 if spp in (16, 32) else 0}, "
     vals, kernel = {}, None
     for f in sorted(glob.glob(os.path.join(a.root, "pmc*", "p*", "*counter_collection.csv"))):
         per = {}
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"]
             # the timed kernel: render_kernel<mode, true, false (no stats), spill>
-            # the timed BVH kernel: render_kernel<layout, true, false (no stats), false (no spill), false, true (on-chip sums), S (node steps)>
+            # the timed BVH kernel: render_kernel<layout, true, false (no stats), false (no spill), false, kAcc (on-chip sums), S (node steps)>
             # (layout 1 for the book cover, 2 for the dense C5 scene)
             if "render_kernel<" not in name or want not in name:
                 continue

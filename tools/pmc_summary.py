@@ -19,10 +19,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # The timed BVH kernel, any LDS layout (1: book cover, 2: dense C5) and step count:
-# render_kernel<L, bvh, stats, progress, spill, on-chip accumulation, S>. The accumulation
-# instance runs when 64 | r (C2-C5); C1 (r = 16) sums through the per-sample buffer.
-KERNELS = {True: ", true, false, false, false, true, ", False: ", true, false, false, false, false, "}
-KERNEL = KERNELS[True]
+# render_kernel<L, bvh, stats, progress, spill, kAcc, S>, kAcc the on-chip accumulation:
+# 1 per 64-sample chunk (64 | r: C2-C5), 2 per pixel-pass (r = 16, 32: C1), 0 none.
+KERNELS = {k: f", true, false, false, false, {k}, " for k in (0, 1, 2)}
+KERNEL = KERNELS[1]
+
+
+def acc_mode(spp):
+    return 1 if spp % 64 == 0 else 2 if spp in (16, 32) else 0
 
 
 def values(path):
@@ -55,15 +59,15 @@ def main():
     d = args.profdir
     # A launch of F frames runs in bands (tray_kernel.hip band_tile_rows), one megakernel
     # dispatch each, and the counters are per dispatch: C2 is one band per 16-frame launch,
-    # C3/C5 several. With on-chip chunk sums (64 | r: C2-C5) a band holds up to
+    # C3/C5 several. With on-chip sums (C1-C5) a band holds up to
     # 2^31 samples, else 2^30 (tray_kernel.hpp kMaxBandSamplesAcc / kMaxBandSamples).
     sys.path.insert(0, ROOT)
     from bench import CONFIGS
 
     _, _, _, W, H, spp, _ = CONFIGS[args.config]
     tiles_x = (W + 7) // 8
-    limit = 1 << (31 if spp % 64 == 0 else 30)
-    KERNEL = KERNELS[spp % 64 == 0]
+    limit = 1 << (31 if acc_mode(spp) else 30)
+    KERNEL = KERNELS[acc_mode(spp)]
     fetch_kb = statistics.median(values(os.path.join(d, "FETCH_SIZE", "pmc_counter_collection.csv")))
     write_kb = statistics.median(values(os.path.join(d, "WRITE_SIZE", "pmc_counter_collection.csv")))
     band_rows = 8 * max(1, limit // (tiles_x * 64 * spp * args.frames))

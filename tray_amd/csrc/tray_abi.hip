@@ -523,15 +523,16 @@ static bool cand_enabled() {
 }
 
 // The fixed-point scale 2^k of a render (tray_kernel.hpp), or 0 for the FP64
-// sum in sample order. Fixed point needs 64 | rays_per_pixel (a 64-item chunk is
-// then one pixel's samples) and a colour bound that leaves k >= kAccMinShift:
+// sum in sample order. Fixed point needs 64 | rays_per_pixel or rays_per_pixel
+// 16 / 32 (acc_groupable: a 64-item chunk is then part of one pixel-pass or
+// whole pixel-passes) and a colour bound that leaves k >= kAccMinShift:
 // a sample's colour is its throughput (a product of <= max_depth attenuations,
 // each <= max_att) times a convex combination of the two background colours,
 // so |c| <= C = max|bg| * max_att^max_depth (x 1.001 for rounding). k is the
 // largest shift with C * 2^k <= 2^kAccBits (tray_kernel.hpp).
 // TRAY_FLAG_ORDERED_SUM selects the FP64 sum in sample order (include/tray.h).
 static int32_t fixed_point_shift(const tray_scene_s* sc, const tray_params* p) {
-    if (p->rays_per_pixel % 64 != 0) return 0;
+    if (!acc_groupable(p->rays_per_pixel)) return 0;
     if (p->flags & TRAY_FLAG_ORDERED_SUM) return 0;
     double bg = 0.0;
     const double comps[6] = {sc->bg_a.x, sc->bg_a.y, sc->bg_a.z, sc->bg_b.x, sc->bg_b.y, sc->bg_b.z};

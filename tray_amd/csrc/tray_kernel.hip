@@ -260,22 +260,31 @@ struct Lane {
     bool busy;
 };
 
-// On-chip accumulation (kAcc; rays per pixel a multiple of 64, so a 64-item
-// chunk is 64 samples of one pixel and one wave takes all of them): the wave
-// keeps kAccCopies sets of three sums per open chunk (a slot) in LDS. A
+// On-chip accumulation (kAcc; rays per pixel r a multiple of 64, so a 64-item
+// chunk is 64 samples of one pixel, or r = 16 / 32, so a chunk is 64 / r whole
+// pixel-passes; one wave takes all of a chunk's items): the wave keeps, per open
+// chunk (a slot) and per pixel-pass group of the chunk, kAccCopies sets of
+// three sums in LDS. A
 // finishing sample adds its rounded, scaled colour there with non-returning
 // LDS atomics (lanes of one wave may finish samples of one chunk in the same
 // instruction; lane l adds to set l % kAccCopies, which halves the same-address
 // serialisation); the adds are exact, so their order does not matter. Slots
 // are retired lazily (acc_retire): when the wave needs a slot and has none
 // free, every open chunk that no busy lane still traces writes its sums to
-// global memory (one 32-B record per 64 samples instead of 24 B per sample)
-// and is freed; at exit the wave retires the rest. No per-sample bookkeeping.
+// global memory (one 32-B record per min(64, r) samples instead of 24 B per
+// sample) and is freed; at exit the wave retires the rest. No per-sample
+// bookkeeping. A sample's group is (item mod 64) >> rshift, with rshift =
+// KernelParams::acc_rshift (6: one group per chunk; log2 r: 64 / r groups).
 typedef __attribute__((address_space(3))) double LdsF64;
 
 struct AccCtx {
-    LdsF64* slabs;  // this wave's slots: kAccCopies x 3 sums each
+    LdsF64* slabs;  // this wave's slots: groups x kAccCopies x 3 sums each
 };
+// kAcc: 1 one group per chunk (64 | r), 2 64 / r pixel-pass groups per chunk (r = 16, 32).
+template <int kAcc>
+__device__ __forceinline__ uint32_t acc_rshift(const KernelParams& p) {
+    return kAcc == 2 ? p.acc_rshift : 6u;
+}
 
 
 // Candidate root of one sphere whose discriminant is >= 0 (Sphere.Hit,
@@ -787,14 +796,16 @@ __device__ __forceinline__ void start_sample(const KernelParams& p, UniPtr uni, 
 // the colour is already scaled by 2^acc_shift (through the background) and is
 // rounded to an integer (tray_kernel.hpp), added with a non-returning LDS
 // atomic (exact, so in any order).
-template <bool kStats, bool kAcc>
+template <bool kStats, int kAcc>
 __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D3& color, Stats& st,
                                          const AccCtx& acc) {
     if constexpr (kAcc) {
 #ifdef TRAY_PROBE_NO_ACC_ADD  // diagnostic only (wrong frames): what the LDS adds cost
         if (color.x != 12345.0) return void(L.busy = false);
 #endif
-        LdsF64* s = acc.slabs + (L.slot * kAccCopies + (threadIdx.x % kAccCopies)) * 3u;
+        const uint32_t rs = acc_rshift<kAcc>(p);
+        const uint32_t group = ((L.slot << (6u - rs)) | ((L.item & 63u) >> rs));
+        LdsF64* s = acc.slabs + (group * kAccCopies + (threadIdx.x % kAccCopies)) * 3u;
         __hip_atomic_fetch_add(s + 0, __builtin_rint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(s + 1, __builtin_rint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(s + 2, __builtin_rint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -877,6 +888,7 @@ __device__ __forceinline__ void write_mean(const KernelParams& p, const double* 
 // Called only when the wave finds no free slot, and at exit: the busy lanes'
 // slots are found by one ballot per open slot. A wave's LDS operations complete
 // in issue order, so the reads see every addition its lanes made.
+template <int kAcc>
 __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccCtx& acc, uint64_t open, bool busy,
                                                uint32_t slot, uint32_t chunk_of, uint32_t lane) {
     uint64_t freed = 0;
@@ -888,19 +900,25 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
     // Lane s retires slot s (chunk_of holds slot s's chunk in lane s): all the
     // wave's retiring slots in one pass. A wave's LDS operations complete in
     // issue order, so the reads see every addition its lanes made.
+    // Each of the slot's groups (one per chunk, or 64 / r pixel-passes) is one record.
     if ((freed >> lane) & 1ull) {
-        volatile LdsF64* v = acc.slabs + lane * kAccCopies * 3u;
-        double sum[3] = {0.0, 0.0, 0.0};  // integers below 2^53: exact in any order
+        const uint32_t groups = 64u >> acc_rshift<kAcc>(p);
+        for (uint32_t g = 0; g < groups; ++g) {
+            const uint32_t slab = kAcc == 1 ? lane : lane * groups + g;
+            volatile LdsF64* v = acc.slabs + slab * kAccCopies * 3u;
+            double sum[3] = {0.0, 0.0, 0.0};  // integers below 2^53: exact in any order
 #pragma unroll
-        for (int k = 0; k < kAccCopies; ++k)
+            for (int k = 0; k < kAccCopies; ++k)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) sum[c] += v[3 * k + c];
+                for (int c = 0; c < 3; ++c) sum[c] += v[3 * k + c];
 #pragma unroll
-        for (int k = 0; k < 3 * kAccCopies; ++k) v[k] = 0.0;
-        AccPartial* o = reinterpret_cast<AccPartial*>(p.samples) + chunk_of;
-        o->sum[0] = sum[0];
-        o->sum[1] = sum[1];
-        o->sum[2] = sum[2];
+            for (int k = 0; k < 3 * kAccCopies; ++k) v[k] = 0.0;
+            AccPartial* o = reinterpret_cast<AccPartial*>(p.samples) + (kAcc == 1 ? chunk_of : chunk_of * groups + g);
+            o->sum[0] = sum[0];
+            o->sum[1] = sum[1];
+            o->sum[2] = sum[2];
+            if constexpr (kAcc == 1) break;
+        }
     }
     return freed;
 }
@@ -914,7 +932,7 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
 // Written for a wave of lanes on different branches: the work several branches
 // need is done once, before them — the bounce's Philox block and the unit
 // direction (sky, Metal, Dielectric).
-template <bool kStats, bool kAcc, typename GeoAt, typename MatAt>
+template <bool kStats, int kAcc, typename GeoAt, typename MatAt>
 __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
                                            double dir_lsq, GeoAt geo_at, MatAt mat_at, Stats& st, const AccCtx& acc) {
     const bool hit = best >= 0;
@@ -1146,9 +1164,10 @@ __host__ __device__ constexpr size_t bvh_stack_bytes(int32_t slots) { return (si
 // LDS with sphere geometry in global memory (scenes too big for 1; BVH only).
 // kProg: the live-progress instance (tray_render_progress only), so the other
 // instances carry no progress code or registers.
-// kAcc: on-chip fixed-point accumulation of each 64-sample chunk (end_path).
+// kAcc: on-chip fixed-point accumulation (end_path): 0 off, 1 one sum per 64-item chunk,
+// 2 one per pixel-pass of a chunk (r = 16, 32).
 // kSteps: node steps per loop iteration at most (kDeepSteps for deep trees, launch_render).
-template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg, bool kAcc, int kSteps = TRAY_NODE_STEPS_MAX>
+template <int kLDS, bool kBVH, bool kStats, bool kSpill, bool kProg, int kAcc, int kSteps = TRAY_NODE_STEPS_MAX>
 __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_SIMD : TRAY_WAVES_PER_SIMD) void render_kernel(KernelParams p) {
     extern __shared__ __attribute__((aligned(16))) double4 smem_all[];
     __attribute__((address_space(3))) Uniforms* uni_lds =
@@ -1221,16 +1240,17 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
         sv.geo = smem;
     }
-    // [acc: waves x acc_slots x kAccSlotBytes] at acc_off
+    // [acc: waves x acc_slots x groups x kAccSlotBytes] at acc_off
     AccCtx acc{nullptr};
     uint64_t acc_free = 0;   // kAcc, wave-uniform: free slots
     uint64_t acc_all = 0;    // kAcc, wave-uniform: every slot
     uint32_t acc_chunk = 0;  // kAcc: lane s holds the chunk of slot s
     if constexpr (kAcc) {
         LdsF64* all = (LdsF64*)reinterpret_cast<double*>(reinterpret_cast<char*>(smem_all) + p.acc_off);
-        const uint32_t waves = blockDim.x / 64u, slots = (uint32_t)p.acc_slots;
-        for (uint32_t i = threadIdx.x; i < waves * slots * kAccCopies * 3u; i += blockDim.x) all[i] = 0.0;
-        acc.slabs = all + (threadIdx.x / 64u) * slots * kAccCopies * 3u;
+        const uint32_t waves = blockDim.x / 64u, slot_f64 = (64u >> acc_rshift<kAcc>(p)) * kAccCopies * 3u;
+        const uint32_t slots = (uint32_t)p.acc_slots;
+        for (uint32_t i = threadIdx.x; i < waves * slots * slot_f64; i += blockDim.x) all[i] = 0.0;
+        acc.slabs = all + (threadIdx.x / 64u) * slots * slot_f64;
         acc_free = acc_all = slots >= 64u ? ~0ull : (1ull << slots) - 1ull;
     }
     __syncthreads();
@@ -1291,7 +1311,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         // Retire the chunks no busy lane traces any more (lanes assigned in
                         // this refill have not started yet: their chunk is open regardless).
                         const bool held = L.busy || fresh_item != ~0u;
-                        acc_free = acc_retire(p, acc, acc_all, held, L.busy ? L.slot : fresh_slot, acc_chunk, lane);
+                        acc_free = acc_retire<kAcc>(p, acc, acc_all, held, L.busy ? L.slot : fresh_slot, acc_chunk, lane);
                     }
                     if (acc_free == 0ull) {
                         // unreachable with nothing in flight: no chunk would hold a slot
@@ -1315,10 +1335,12 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 pool_next = c * 64u;
                 pool_end = pool_next + 64u;
                 if constexpr (kAcc) {
-                    // Every item of a chunk is one pixel's (64 | r): valid or padding together.
+                    // With 64 | r every item of a chunk is one pixel's: valid or padding
+                    // together. A chunk of several pixel-passes (r | 64) may mix the two
+                    // and always takes a slot (its padding groups retire as zeros).
                     int32_t cx, cj;
                     uint32_t cs, cp;
-                    if (pool_next < p.items && decode_item(p, pool_next, cx, cj, cs, cp)) {
+                    if (acc_rshift<kAcc>(p) < 6u || (pool_next < p.items && decode_item(p, pool_next, cx, cj, cs, cp))) {
                         pool_slot = (uint32_t)__builtin_ctzll(acc_free);
                         acc_free &= ~(1ull << pool_slot);
                         acc_chunk = lane == pool_slot ? c : acc_chunk;
@@ -1596,7 +1618,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         }
     }
     if constexpr (kProg) flush_progress(p, prog_cur, prog_cnt, lane);
-    if constexpr (kAcc) (void)acc_retire(p, acc, acc_all & ~acc_free, false, 0u, acc_chunk, lane);  // every lane is idle
+    if constexpr (kAcc) (void)acc_retire<kAcc>(p, acc, acc_all & ~acc_free, false, 0u, acc_chunk, lane);  // every lane is idle
     if constexpr (kStats) {
         atomicAdd(p.stats + 0, (unsigned long long)st.segments);
         atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
@@ -1691,10 +1713,11 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
     D3 sum = d3(0, 0, 0);
     if constexpr (kMode == kResolvePartials) {
         if (!valid) return;
-        const AccPartial* part = reinterpret_cast<const AccPartial*>(p.samples) + (item0 >> 6);
+        // One record per 64 items (64 | r: r / 64 per pixel-pass) or per pixel-pass (r | 64).
+        const AccPartial* part = reinterpret_cast<const AccPartial*>(p.samples) + (item0 >> p.acc_rshift);
         int64_t s[3] = {0, 0, 0};
         uint32_t bad = 0u;
-        for (int32_t c = 0; c < p.spp / 64; ++c)
+        for (int32_t c = 0; c < (p.spp >> p.acc_rshift); ++c)
 #pragma unroll
             for (int k = 0; k < 3; ++k) acc_add(part[c].sum[k], 0x1p53, s[k], bad, k);
         write_acc_mean<kFmt>(p, srgb, s, bad, x, j, pass);
@@ -1915,23 +1938,28 @@ hipError_t launch_to_srgba(const double* rgb, size_t n_pixels, uint32_t* rgba, c
 
 using KernelFn = void (*)(KernelParams);
 
-template <bool kBVH, bool kSpill, bool kStats, bool kProg, bool kAcc, int kSteps>
+template <bool kBVH, bool kSpill, bool kStats, bool kProg, int kAcc, int kSteps>
 static KernelFn pick_kernel4(int lds_mode) {
-    if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
-    if constexpr (kBVH)
-        if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
-    return render_kernel<0, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
+    if constexpr (kAcc == 2) {  // pixel-pass groups: only with the whole scene in LDS (launch_layout)
+        (void)lds_mode;
+        return render_kernel<1, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
+    } else {
+        if (lds_mode == 1) return render_kernel<1, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
+        if constexpr (kBVH)
+            if (lds_mode == 2) return render_kernel<2, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
+        return render_kernel<0, kBVH, kStats, kSpill, kProg, kAcc, kSteps>;
+    }
 }
-template <bool kBVH, bool kSpill, bool kStats, bool kProg, bool kAcc>
+template <bool kBVH, bool kSpill, bool kStats, bool kProg, int kAcc>
 static KernelFn pick_kernel3(int lds_mode, bool deep) {
-    if constexpr (kBVH && !kSpill)
+    if constexpr (kBVH && !kSpill && kAcc != 2)
         if (deep) return pick_kernel4<kBVH, kSpill, kStats, kProg, kAcc, kDeepSteps>(lds_mode);
     return pick_kernel4<kBVH, kSpill, kStats, kProg, kAcc, TRAY_NODE_STEPS_MAX>(lds_mode);
 }
 
 // Instrumentation: the stats instance counts segments and tests; the progress
 // instance feeds tray_render_progress; neither is ever timed by the bench.
-template <bool kBVH, bool kSpill, bool kAcc>
+template <bool kBVH, bool kSpill, int kAcc>
 static KernelFn pick_kernel2(int lds_mode, bool stats, bool progress, bool deep) {
     if (stats) return pick_kernel3<kBVH, kSpill, true, false, kAcc>(lds_mode, deep);
     if (progress) return pick_kernel3<kBVH, kSpill, false, true, kAcc>(lds_mode, deep);
@@ -1941,11 +1969,12 @@ static KernelFn pick_kernel2(int lds_mode, bool stats, bool progress, bool deep)
 // On-chip accumulation is built for the BVH kernel with the whole stack on
 // chip (launch_layout grants accumulators only then); every other launch sums
 // through the per-sample buffer.
-static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, bool spill, bool acc, bool deep) {
-    if (!bvh) return pick_kernel2<false, false, false>(lds_mode, stats, progress, false);
-    if (spill) return pick_kernel2<true, true, false>(lds_mode, stats, progress, false);
-    return acc ? pick_kernel2<true, false, true>(lds_mode, stats, progress, deep)
-               : pick_kernel2<true, false, false>(lds_mode, stats, progress, deep);
+static KernelFn pick_kernel(int lds_mode, bool bvh, bool stats, bool progress, bool spill, int acc, bool deep) {
+    if (!bvh) return pick_kernel2<false, false, 0>(lds_mode, stats, progress, false);
+    if (spill) return pick_kernel2<true, true, 0>(lds_mode, stats, progress, false);
+    if (acc == 2) return pick_kernel2<true, false, 2>(lds_mode, stats, progress, false);
+    return acc == 1 ? pick_kernel2<true, false, 1>(lds_mode, stats, progress, deep)
+                    : pick_kernel2<true, false, 0>(lds_mode, stats, progress, deep);
 }
 
 template <int kMode>
@@ -2037,24 +2066,25 @@ static int32_t band_tile_rows(int32_t width, uint64_t spp, bool partials) {
 }
 
 // Bytes of the buffer one band of `band_tiles` tile rows needs: a colour per sample, or
-// one chunk record per 64 samples (partials).
-static size_t band_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials, int32_t band_tiles) {
+// one chunk record per 2^rshift samples (partials).
+static size_t band_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials, int32_t band_tiles,
+                                uint32_t rshift = 6) {
     if (rows <= 0) return 0;
     const int32_t tile_rows = std::min(band_tiles, (rows + 7) / 8);
     const size_t samples = (size_t)((width + 7) / 8) * 64u * (size_t)tile_rows * (size_t)spp;
-    return partials ? samples / 64u * sizeof(AccPartial) : samples * 3 * sizeof(double);
+    return partials ? (samples >> rshift) * sizeof(AccPartial) : samples * 3 * sizeof(double);
 }
 
 size_t sample_buffer_bytes(int32_t width, int32_t rows, uint64_t spp) {
     return band_buffer_bytes(width, rows, spp, false, band_tile_rows(width, spp, false));
 }
 
-size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials) {
-    return band_buffer_bytes(width, rows, spp, partials, band_tile_rows(width, spp, partials));
+size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials, uint32_t rshift) {
+    return band_buffer_bytes(width, rows, spp, partials, band_tile_rows(width, spp, partials), rshift);
 }
 
 LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
-    LaunchLayout L{0, 0, 0, 0, 0};
+    LaunchLayout L{0, 0, 0, 0, 0, 6u};
     if (use_bvh) {
         // Whole scene in LDS when it fits next to kStackLdsMin stack slots, else
         // the nodes and leaf table when they fit, else nothing; the stack then
@@ -2076,9 +2106,11 @@ LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
             L.stack_lds = std::min(L.stack_lds, (int32_t)std::max<long long>(kStackLdsMin, std::min<long long>(knob, 1 << 20)));
         L.lds = kUniformsBytes + bvh_stack_bytes(L.stack_lds) + scene;
         // Chunk accumulators in what the whole stack leaves (fixed-point frames only).
-        if (p.acc_shift > 0 && L.stack_lds == p.stack_cap && p.spp % 64 == 0) {
+        if (p.acc_shift > 0 && L.stack_lds == p.stack_cap && acc_groupable(p.spp) &&
+            (acc_record_shift(p.spp) == 6u || L.lds_mode == 1)) {  // groups: one kernel instance (scene in LDS)
+            const uint32_t rshift = acc_record_shift(p.spp);
             const size_t waves = (size_t)kBvhBlock / 64u;
-            const size_t per_slot = waves * kAccSlotBytes;
+            const size_t per_slot = waves * kAccSlotBytes * (64u >> rshift);  // every group of a chunk
             const size_t left = kMaxLDSBytes - L.lds;
             int32_t slots = (int32_t)std::min<size_t>(kAccSlotsMax, left / per_slot);
             const bool forced = debug_knob(kKnobAccSlots, &knob);  // tests / A-B: fewer slots, 0 = off
@@ -2086,6 +2118,7 @@ LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
             if (slots >= kAccSlotsMin || (slots > 0 && forced)) {
                 L.acc_slots = slots;
                 L.acc_off = (uint32_t)L.lds;
+                L.acc_rshift = rshift;
                 L.lds += (size_t)slots * per_slot;
             }
         }
@@ -2107,7 +2140,7 @@ LaunchPlan plan_launch(const KernelParams& p, bool use_bvh) {
     const uint64_t spp_launch = (uint64_t)p.spp * std::max<uint32_t>(p.passes, 1u);
     const bool partials = L.layout.acc_slots > 0;
     L.band_tiles = band_tile_rows(p.width, spp_launch, partials);
-    L.buffer_bytes = band_buffer_bytes(p.width, p.rows, spp_launch, partials, L.band_tiles);
+    L.buffer_bytes = band_buffer_bytes(p.width, p.rows, spp_launch, partials, L.band_tiles, L.layout.acc_rshift);
     return L;
 }
 
@@ -2125,13 +2158,14 @@ hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, h
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    if (p.acc_shift > 0 && p.spp % 64 != 0) return hipErrorInvalidValue;  // the caller decides (fixed_point_shift)
+    if (p.acc_shift > 0 && !acc_groupable(p.spp)) return hipErrorInvalidValue;  // the caller decides (fixed_point_shift)
     const LaunchLayout& layout = plan.layout;
     const int lds_mode = layout.lds_mode;
     const size_t lds = layout.lds;
     p.stack_lds = layout.stack_lds;
     p.acc_slots = layout.acc_slots;
     p.acc_off = layout.acc_off;
+    p.acc_rshift = layout.acc_rshift;
     if (use_bvh && p.stack_cap > p.stack_lds && !p.stack_ovf) return hipErrorInvalidValue;
     // The caller sized p.samples from this plan (an invariant: the plan is decided once).
     const int32_t band_tiles = plan.band_tiles;
@@ -2143,7 +2177,8 @@ hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, h
     if (debug_knob(kKnobNodeDeep, &knob))  // A/B: force the instance
         deep = use_bvh && knob != 0;
     const KernelFn fn = pick_kernel(lds_mode, use_bvh, stats, p.progress != nullptr,
-                                    use_bvh && p.stack_cap > p.stack_lds, p.acc_slots > 0, deep);
+                                    use_bvh && p.stack_cap > p.stack_lds,
+                                    p.acc_slots <= 0 ? 0 : p.acc_rshift < 6u ? 2 : 1, deep);
     const KernelFn resolve = pick_resolve(p);
     // Per-device, per-(kernel, LDS size) launch setup, cached.
     struct Setup {

@@ -101,12 +101,13 @@ struct KernelParams {
     FastDiv div_spp, div_tiles_x, div_tile_rows;  // item decoding; compact row -> image row
     double* samples;     // per-item path colours (3 doubles), summed by the resolve kernel; with
                          // on-chip accumulation (acc_slots > 0) the same buffer holds AccPartial records
-    // Fixed-point accumulation (acc_shift > 0, rays_per_pixel a multiple of 64):
+    // Fixed-point accumulation (acc_shift > 0, rays_per_pixel a multiple of 64 or 16 / 32):
     // the background is pre-scaled by 2^acc_shift, each sample's scaled colour is rounded to
     // an integer and the integers are summed exactly (order-free); 0: FP64 sum in sample order.
     int32_t acc_shift;
     int32_t acc_slots;   // >0: per-wave LDS accumulators (slots per wave), partial per 64-item chunk
     uint32_t acc_off;    // byte offset of the accumulator region in the kernel's dynamic LDS
+    uint32_t acc_rshift;  // items per chunk record = 2^acc_rshift: 6 (64 | r) or log2 r (r = 16, 32)
     const Bvh4Node* nodes;  // exact-culling 4-wide BVH (tray_bvh.cpp), root first
     const int32_t* leaves;  // per leaf: (first slot << 3) | count
     int32_t leaf_single;    // 1: every leaf holds one sphere and its index is its slot
@@ -177,10 +178,18 @@ struct LaunchLayout {
     size_t lds;
     int32_t acc_slots;  // 0: accumulate through the per-sample buffer
     uint32_t acc_off;
+    uint32_t acc_rshift;  // KernelParams::acc_rshift (6 when acc_slots is 0)
 };
+// Rays per pixel whose samples can be summed in fixed point, on chip: 64 | r (a
+// 64-item chunk is one pixel-pass's samples, or part of them) or r = 16 / 32 (a
+// chunk is 64 / r whole pixel-passes). Smaller r would leave too few slots.
+constexpr bool acc_groupable(int32_t spp) { return spp > 0 && (spp % 64 == 0 || spp == 16 || spp == 32); }
+// log2 of the items per chunk record for rays per pixel `spp`.
+constexpr uint32_t acc_record_shift(int32_t spp) { return spp % 64 == 0 ? 6u : spp == 32 ? 5u : 4u; }
 LaunchLayout launch_layout(const KernelParams& p, bool use_bvh);
-// Device bytes of the per-sample buffer or (acc_slots > 0) the chunk partials.
-size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials);
+// Device bytes of the per-sample buffer or (acc_slots > 0) the chunk partials
+// (one per 2^rshift samples).
+size_t accum_buffer_bytes(int32_t width, int32_t rows, uint64_t spp, bool partials, uint32_t rshift = 6);
 // Everything a launch decides from p and the debug knobs, decided ONCE
 // (plan_launch) and handed to launch_render, so the buffer the caller sizes
 // from it and the bands the launch runs cannot disagree.
