@@ -527,10 +527,10 @@ def main() -> int:
                          "peak = 78.6 TFLOP/s FP64 vector spec / 2 = 39.3 T ops/s",
             "algorithmic_bytes_per_launch": alg_bytes,
             "traffic_over_algorithmic": round(traffic / alg_bytes, 2) if traffic else None,
-            "traffic_note": "megakernel HBM bytes by PMC (FETCH_SIZE x2 + WRITE_SIZE). With 64 | r each pixel's "
-                            "samples are summed exactly in LDS as fixed-point integers and the megakernel writes one "
-                            "32-B record per 64-sample chunk (DESIGN.md 5, Accumulation); the resolve pass turns them "
-                            "into the frames",
+            "traffic_note": "megakernel HBM bytes by PMC (FETCH_SIZE x2 + WRITE_SIZE). With 64 | r (or r = 16, 32) "
+                            "each pixel's samples are summed exactly in LDS as fixed-point integers and the megakernel "
+                            "writes one 32-B record per 64-sample chunk (per pixel-pass at r = 16, 32; DESIGN.md 5, "
+                            "Accumulation); the resolve pass turns them into the frames",
             "traversal": "linear scan" if args.linear else "exact-culling 4-wide BVH; camera rays: per-pixel "
                                                             "candidate lists (no traversal)",
             "ops_note": "achieved counts the work executed: the candidate lists removed ~35 % of the box tests "
