@@ -202,3 +202,32 @@ def test_environment_is_ignored(L, O):
         os.environ.clear()
         os.environ.update(old)
         dev.release()
+
+
+@pytest.mark.parametrize("spp", [16, 32])
+def test_pixel_pass_sums_in_every_instance(L, O, spp):
+    """r = 16 / 32 (one on-chip record per pixel-pass) in the plain, live-progress and
+    counting kernel instances: the same frame, and the counted segments equal the
+    oracle's Scene.Hit calls."""
+    import torch
+
+    sc = O.rich_scene(2)
+    w, h, depth = 37, 21, 50
+    st = camera(L, RICH_SETUP, w, h)
+    p = L.make_params(w, h, depth, spp, 0.5, 7, output=L.OUT_RGB_F32)
+    plain, _ = L.render(sc, bg_struct(L, DEFAULT_BG), st, p, 0)
+    rows = []
+    live, _ = L.render(sc, bg_struct(L, DEFAULT_BG), st, p, 0, progress=rows.append)
+    assert np.array_equal(plain, live) and sum(rows) == h
+    dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
+    try:
+        assert dev.plan(st, p, 1).acc_slots > 0
+        out = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+        stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+        dev.render_stats_async(st, p, out.data_ptr(), stats.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), plain)
+    finally:
+        dev.release()
+    _, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, spp, depth, 0.5, 7, workers=WORKERS)
+    assert int(stats[0]) == int(rseg.sum())
