@@ -417,7 +417,7 @@ def main() -> int:
     set_phase("launch timings")
     kernel_ms = launch_ms(F)  # the timed launch shape: F frames, megakernel + F resolves
     single_ms = kernel_ms if F == 1 else None if args.no_single else launch_ms(1)  # one frame, nothing overlapped
-    ranks_rec = None
+    ranks_rec = parity_n = None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -445,6 +445,20 @@ def main() -> int:
                      "gather_ms_per_launch_max": max(r["gather_ms_per_launch"] for r in allr),
                      "what": "untimed: one launch of F frames of each rank's rows (HIP events) and one gather of "
                              "F frames to rank 0 (HIP events on the gather stream); ms_per_step is the timed run"}
+        if not args.no_cpu_baseline:
+            # Untimed: is the frame the N ranks assemble the right image? Every rank renders
+            # pass 0 again in the timed shape and as FP64 with segment counts; all three are
+            # gathered to rank 0, which checks them against the oracle (ray/tracer.go:86-116
+            # splits rows over goroutines; here over ranks, and the pixels must not change).
+            set_phase("gathered-frame parity")
+            torch.cuda.synchronize()
+            dist.barrier()
+            gathered = gather_pass0(torch, _lib, shard, scene, cam, params, F, launch, outs[0], gather_for(0, F),
+                                    args.tile_rows, world, rank)
+            if rank == 0:
+                row_step = args.cpu_row_step or auto_row_step(len(spheres), W, H, spp)
+                parity_n = gathered_parity(gathered, spheres, cam._state.as_array(), W, H, spp, depth, seed, row_step)
+            dist.barrier()
 
     samples = W * H * spp
     value = samples * args.steps / elapsed / 1e6
@@ -573,10 +587,11 @@ def main() -> int:
             rec["cpu_baseline"], ref = cpu_baseline(spheres, cam._state.as_array(), W, H, spp, depth, seed, row_step,
                                                     args.cpu_min_seconds)
             rec["parity"] = device_parity(torch, _lib, scene, cam, params, F, launch, outs[0], ref, row_step)
+        elif parity_n is not None:
+            rec["parity"] = parity_n
         else:
             rec["parity"] = None
-            rec["parity_null_reason"] = ("measured at N = 1 (the oracle frame is cpu_baseline's)" if world > 1
-                                         else "--no-cpu-baseline: no oracle frame")
+            rec["parity_null_reason"] = "--no-cpu-baseline: no oracle frame"
     if rank == 0:
         print(json.dumps(rec), flush=True)
     set_phase("teardown")
@@ -663,7 +678,10 @@ def cpu_baseline(spheres, camera, W, H, spp, depth, seed, row_step, min_seconds=
     ray/tracer.go:86-116) on every `row_step`-th row of the same frame, pass 0;
     while less than `min_seconds` have passed, passes 1, 2, ... of the same rows
     (a frame as small as C1's renders in well under a second). Returns the
-    record and pass 0's (rows, segments) for the parity check."""
+    record and pass 0's (rows, segments) for the parity check. Pass 0 is timed
+    with segments=True: the oracle counts every path's Scene.Hit calls whether or
+    not they are asked for (tray_oracle.c render_pixel), the flag only stores one
+    uint32 per pixel, so the timed work is the same as with segments=False."""
     from oracle import oracle as O
 
     cores, why = cpu_share()
@@ -704,6 +722,57 @@ def frame_parity(ref, ref_seg, f64, seg, f32, tol=1e-4):
            "f32_equal_frac": round(float((g32 == ref.astype(np.float32)).mean()), 4),
            "tol": tol}
     rec["ok"] = bool(rec["segments_equal"] and linf <= tol and linf32 <= tol and np.isfinite(ref).all())
+    return rec
+
+
+def gather_pass0(torch, _lib, shard, scene, cam, params, F, launch, out, gather32, tile_rows, world, rank):
+    """N > 1, every rank (untimed): pass 0 of its rows (a) as frame 0 of a passes
+    launch in the timed shape (slot 0, F frames, TRAY_OUT_RGB_F32) gathered to rank 0
+    by the timed frames' own FrameGather, and (b) through tray_render_async as
+    TRAY_OUT_RGB_F64 with per-pixel Scene.Hit counts, gathered likewise. Returns
+    rank 0's assembled (f64 [H, W, 3], segments [H, W], f32 [H, W, 3]) as numpy,
+    None on the other ranks."""
+    W, H = params.width, params.height
+    rows = _lib.params_rows(params)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    p = _lib.Params.from_buffer_copy(params)
+    p.output, p.pass_ = _lib.OUT_RGB_F64, 0
+    f64 = torch.empty((1, rows, W, 3), dtype=torch.float64, device=dev)
+    seg = torch.zeros((1, rows, W), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    scene.render_async(cam._state, p, f64.data_ptr(), seg.data_ptr(), stream.cuda_stream)
+    with torch.cuda.stream(stream):
+        launch(0, 0, F)  # frames 0 .. F-1 of this rank's rows, as the timed launches render them
+    torch.cuda.synchronize()
+    g32 = gather32(out[:F])
+    g64 = shard.FrameGather(1, H, W, (3,), tile_rows, world, rank, torch.float64, dev)(f64)
+    gseg = shard.FrameGather(1, H, W, (), tile_rows, world, rank, torch.int32, dev)(seg)
+    torch.cuda.synchronize()
+    if rank != 0:
+        return None
+    return (g64[0].cpu().numpy(), gseg[0].cpu().numpy().astype(np.uint32), g32[0].cpu().numpy())
+
+
+def gathered_parity(gathered, spheres, camera, W, H, spp, depth, seed, row_step, workers=None):
+    """N > 1, rank 0: the frame the ranks assembled (gather_pass0) against the
+    oracle's pass 0 on every `row_step`-th row (the rows cpu_baseline renders at
+    N = 1), with frame_parity's bar: segment counts bit-exact, L-inf <= 1e-4."""
+    from oracle import oracle as O
+
+    f64, seg, f32 = gathered
+    rows = np.arange(0, H, row_step, dtype=np.int32)
+    cores = workers or cpu_share()[0]
+    t0 = time.perf_counter()
+    ref, ref_seg = O.render_rows(spheres, np.array([1.0, 1.0, 1.0, 0.4, 0.65, 1.0]), camera, W, H, spp, depth, 0.5,
+                                 seed, rows, workers=cores, segments=True)
+    rec = frame_parity(ref, ref_seg, f64[rows], seg[rows], f32[rows])
+    rec.update({"pass": 0, "oracle_seconds": round(time.perf_counter() - t0, 2),
+                "scope": ("the whole gathered frame" if row_step == 1 else
+                          f"every {row_step}. row of the gathered frame ({len(rows)} of {H} rows)"),
+                "frame": "assembled on rank 0 from every rank's row tiles by the timed run's gather "
+                         "(shard.FrameGather), f32 frame 0 of a passes launch and an f64 render with segment counts",
+                "reference": "oracle/tray_oracle.c (ray/*.go restated; per-pixel parity with the Go binary's "
+                             "fortio.org/rand stream is unpinned, DESIGN.md 3)"})
     return rec
 
 

@@ -276,8 +276,10 @@ int tray_render_devices_progress(const tray_sphere *spheres, int32_t n_spheres, 
  * candidate records and traversal-stack overflow area) for as long as it runs:
  * the one last used on the same stream, else an idle one, else a new one (up to
  * 4 per scene), else the least recently used, which the new render's stream
- * then waits for on the device (hipStreamWaitEvent). Buffers grow only after
- * the renders using them have finished. Results do not depend on which context
+ * then waits for on the device (hipStreamWaitEvent). A buffer that must grow is
+ * freed and reallocated in the new render's stream order (hipFreeAsync /
+ * hipMallocAsync), after the renders using it: the async calls only enqueue,
+ * they never wait for the device. Results do not depend on which context
  * a render takes. tray_scene_release waits for the scene's enqueued renders and
  * must not race with a call still enqueueing on the same handle. */
 int tray_scene_upload(const tray_sphere *spheres, int32_t n_spheres, const tray_background *background,

@@ -30,8 +30,10 @@
  *                         scene beyond this many in flight wait for the least
  *                         recently used one; 1 serialises them (same bits)
  *   "grid_reserve"        workgroup slots the persistent render grid leaves
- *                         free on the device (0..CUs-1), for kernels that run
- *                         beside it: collectives, copies (same bits)
+ *                         free, out of the workgroups the device keeps resident
+ *                         for the kernel instance (several per CU for small
+ *                         instances; clamped to 0..resident-1), for kernels
+ *                         that run beside it: collectives, copies (same bits)
  */
 #ifndef TRAY_DEBUG_H
 #define TRAY_DEBUG_H

@@ -60,6 +60,16 @@ def load_golden(name):
     return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
 
 
+def example_sky_mask():
+    """tests/golden/example_sky_mask.npz: the pixels of example.png no camera ray of
+    any RichScene can reach a sphere from (tests/golden/make_sky_mask.py), their
+    bytes in row-major order, and the rows to render to cover them."""
+    g = load_golden("example_sky_mask")
+    h, w = (int(v) for v in g["shape"])
+    mask = np.unpackbits(g["mask"])[: h * w].reshape(h, w).astype(bool)
+    return mask, g["rgb"], int(np.nonzero(mask.any(1))[0].max()) + 1
+
+
 RICH_SETUP = np.array([13, 2, 3, 0, 0, 0, 0, 1, 0, 20.0, 10.0, 10.0, 0.1])  # RichSceneCamera, camera.go:144-154
 DEFAULT_BG = np.array([1.0, 1.0, 1.0, 0.4, 0.65, 1.0])  # DefaultBackground, objects.go:106-110
 

@@ -219,6 +219,35 @@ def test_example_png_sky_rows(L, O):
     assert np.array_equal(d0[~near], np.zeros_like(d0[~near]))
 
 
+def test_example_png_sky_mask(L, O):
+    """example.png's scene-independent sky (tests/golden/make_sky_mask.py: 145,582
+    pixels of rows 0..156 no ray of any RichScene's camera footprint can reach a
+    sphere from) on the device, under the rules of test_example_png_sky_rows."""
+    from conftest import example_sky_mask
+
+    mask, rgb, ymax = example_sky_mask()
+    m = mask[:ymax]
+    sc = O.rich_scene(2)
+    st = camera(L, RICH_SETUP, 1280, 720)
+    u8, seg = gpu_render(L, sc, DEFAULT_BG, st, 1280, 720, 64, 50, 0.5, 2, y_start=0, y_end=ymax,
+                         output=L.OUT_RGBA8)
+    assert np.all(seg[m] == 64)
+    d = np.abs(u8[..., :3][m].astype(int) - rgb.astype(int))
+    assert d.max() <= 1 and (d.max(-1) == 0).mean() >= 0.98
+    lin, _ = gpu_render(L, sc, DEFAULT_BG, st, 1280, 720, 64, 50, 0.5, 2, y_start=0, y_end=ymax)
+    assert np.array_equal(O.to_srgba(lin), u8)
+    assert not np.any((d > 0) & (srgb_boundary_distance(lin)[m] >= SKY_EDGE_AA))
+    setup = RICH_SETUP.copy()
+    setup[12] = 0.0
+    st0 = camera(L, setup, 1280, 720)
+    lin0, seg0 = gpu_render(L, sc, DEFAULT_BG, st0, 1280, 720, 1, 50, 0.5, 2, y_start=0, y_end=ymax)
+    assert np.all(seg0[m] == 1)
+    d0 = np.abs(O.to_srgba(lin0)[..., :3][m].astype(int) - rgb.astype(int))
+    near = srgb_boundary_distance(lin0)[m] < SKY_EDGE_PINHOLE
+    assert d0.max() <= 1 and near.mean() < 0.05
+    assert np.array_equal(d0[~near], np.zeros_like(d0[~near]))
+
+
 def test_config2_full_size_properties(L, O):
     """BASELINE config 2 at full size (1280x720, r=64, d=50): determinism, and a
     random spot-check of pixels against the oracle (size-independent parity)."""

@@ -7,7 +7,8 @@ import os
 import numpy as np
 import pytest
 
-from conftest import SKY_EDGE_AA, SKY_EDGE_PINHOLE, srgb_boundary_distance, DEFAULT_BG, RICH_SETUP, load_golden
+from conftest import (DEFAULT_BG, RICH_SETUP, SKY_EDGE_AA, SKY_EDGE_PINHOLE, example_sky_mask, load_golden,
+                      srgb_boundary_distance)
 
 
 def test_unit_vector_distribution(O):  # ray/vec3_test.go:539-649 (100k samples)
@@ -93,6 +94,33 @@ def test_example_png_sky_rows(O):
     assert d0.max() <= 1 and (d0.max(-1) == 0).mean() >= 0.985
     near = srgb_boundary_distance(img0) < SKY_EDGE_PINHOLE
     assert near.mean() < 0.03  # the exemption covers < 3 % of channels
+    assert np.array_equal(d0[~near], np.zeros_like(d0[~near]))
+
+
+def test_example_png_sky_mask(O):
+    """145,582 pixels of the reference's own output (rows 0..156: the sky above the
+    horizon, and below it where rays descend too little to meet the R=1000 ground,
+    between and above the spheres), pinned with example_sky_rows' rules: every
+    sample escapes at its first segment, the r=64 frame differs by at most 1 LSB
+    and only next to an encoder rounding boundary, the pixel-centre pinhole frame
+    is exact except within SKY_EDGE_PINHOLE of a boundary."""
+    mask, rgb, ymax = example_sky_mask()
+    assert mask.sum() >= 120_000 and mask[:49].all()
+    _, cam = O.camera_initialize(RICH_SETUP, 1280, 720)
+    img, seg = O.render(O.rich_scene(2), DEFAULT_BG, cam, 1280, 720, 64, 50, 0.5, 2, 0, ymax,
+                        workers=os.cpu_count() or 4)
+    m = mask[:ymax]
+    assert np.all(seg[m] == 64)
+    diff = np.abs(O.to_srgba(img)[..., :3][m].astype(int) - rgb.astype(int))
+    assert diff.max() <= 1 and (diff.max(-1) == 0).mean() >= 0.98
+    assert not np.any((diff > 0) & (srgb_boundary_distance(img)[m] >= SKY_EDGE_AA))
+    setup = RICH_SETUP.copy()
+    setup[12] = 0.0
+    _, cam0 = O.camera_initialize(setup, 1280, 720)
+    img0, _ = O.render(None, DEFAULT_BG, cam0, 1280, 720, 1, 50, 0.5, 2, 0, ymax)
+    d0 = np.abs(O.to_srgba(img0)[..., :3][m].astype(int) - rgb.astype(int))
+    near = srgb_boundary_distance(img0)[m] < SKY_EDGE_PINHOLE
+    assert d0.max() <= 1 and near.mean() < 0.05
     assert np.array_equal(d0[~near], np.zeros_like(d0[~near]))
 
 

@@ -493,9 +493,9 @@ int tray_scene_get_info(tray_scene_t sc, tray_scene_info* out) {
 static void free_ctx(LaunchCtx* c) {
     if (c->launched) (void)hipEventSynchronize(c->done);  // its last render, on whatever stream
     if (c->queue) (void)hipFree(c->queue);
-    if (c->samples) (void)hipFree(c->samples);
-    if (c->cand) (void)hipFree(c->cand);
-    if (c->stack_ovf) (void)hipFree(c->stack_ovf);
+    // Pool allocations (grow_ctx_buffer), idle now: released on the null stream.
+    for (void* b : {(void*)c->samples, (void*)c->cand, (void*)c->stack_ovf})
+        if (b) (void)hipFreeAsync(b, nullptr);
     if (c->done) (void)hipEventDestroy(c->done);
     delete c;
 }
@@ -667,21 +667,27 @@ static int take_ctx(tray_scene_t sc, hipStream_t stream, LaunchCtx** out) {
     return TRAY_OK;
 }
 
-// Grows a context buffer to `bytes` (contents not kept). The context's last
-// render may still run on another stream: wait for it before freeing.
-static hipError_t grow_ctx_buffer(LaunchCtx* c, void** buf, size_t* have, size_t bytes) {
+// Grows a context buffer to `bytes` (contents not kept) in the order of the
+// render's `stream`, without blocking the host: the old buffer goes back with
+// hipFreeAsync on `stream`, which take_ctx has already ordered after the
+// context's last render (hipStreamWaitEvent on its event, or stream order when
+// that render ran on `stream`), and the new one comes from the device's
+// stream-ordered pool (hipMallocAsync). A plain hipFree synchronises the whole
+// device on ROCm: under the scene's mutex it held this thread, and every other
+// thread enqueueing on the scene, until the longest render in flight ended
+// (include/tray.h presents the async calls as enqueue-only). Every context
+// buffer is a pool allocation, so free_ctx releases them the same way.
+static hipError_t grow_ctx_buffer(void** buf, size_t* have, size_t bytes, hipStream_t stream) {
     if (*have >= bytes) return hipSuccess;
     if (*buf) {
-        if (c->launched) {
-            const hipError_t e = hipEventSynchronize(c->done);
-            if (e != hipSuccess) return e;
-        }
-        (void)hipFree(*buf);
+        const hipError_t e = hipFreeAsync(*buf, stream);
+        if (e != hipSuccess) return e;
         *buf = nullptr;
         *have = 0;
     }
-    const hipError_t e = hipMalloc(buf, bytes);
+    const hipError_t e = hipMallocAsync(buf, bytes, stream);
     if (e == hipSuccess) *have = bytes;
+    else *buf = nullptr;
     return e;
 }
 
@@ -723,9 +729,9 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         }
         return TRAY_OK;
     };
-    hipError_t e = grow_ctx_buffer(c, reinterpret_cast<void**>(&c->samples), &c->samples_bytes, plan.buffer_bytes);
+    hipError_t e = grow_ctx_buffer(reinterpret_cast<void**>(&c->samples), &c->samples_bytes, plan.buffer_bytes, stream);
     if (e == hipSuccess && use_bvh && k.stack_cap > plan.layout.stack_lds)
-        e = grow_ctx_buffer(c, reinterpret_cast<void**>(&c->stack_ovf), &c->ovf_bytes, sc->ovf_bytes);
+        e = grow_ctx_buffer(reinterpret_cast<void**>(&c->stack_ovf), &c->ovf_bytes, sc->ovf_bytes, stream);
     if (e != hipSuccess) return finish(e, "launch context buffers");
     k.queue = c->queue;
     k.samples = c->samples;
@@ -740,8 +746,8 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         key.multi_sample = p->rays_per_pixel > 1;
         if (!c->cand_valid || memcmp(&key, &c->cand_key, sizeof(key)) != 0) {
             c->cand_valid = false;
-            e = grow_ctx_buffer(c, reinterpret_cast<void**>(&c->cand), &c->cand_bytes,
-                                cand_workspace_bytes(p->width, k.rows));
+            e = grow_ctx_buffer(reinterpret_cast<void**>(&c->cand), &c->cand_bytes,
+                                cand_workspace_bytes(p->width, k.rows), stream);
             if (e == hipSuccess) e = launch_cand_build(k, c->cand, stream);
             if (e != hipSuccess) return finish(e, "candidate lists");
             c->cand_key = key;

@@ -1145,6 +1145,15 @@ __device__ __forceinline__ void prof_material(int site, bool active, int32_t slo
 #define PROF_MATERIAL(site, active)
 #endif
 
+// Diagnostic build only (-DTRAY_PROFILE_TIMELINE, stats instance; tools/timeline.py):
+// per wave, busy lanes integrated over time in kTlTicks buckets of the 100 MHz
+// constant clock, relative to the wave's start, plus its start, end, the time its
+// queue ran dry and the chunks it took. Record of wave w at stats[32 + w x kTlStride]:
+// [0] start, [1] end, [2] exhausted (ticks after start), [3] chunks, [4..] buckets.
+#ifdef TRAY_PROFILE_TIMELINE
+constexpr uint32_t kTlBuckets = 1024, kTlTicks = 1000, kTlStride = kTlBuckets + 4;  // 10-us buckets
+#endif
+
 // Persistent megakernel: waves pull 64-pixel work items from a global counter
 // and lanes refill individually, so no lane idles while the frame has work.
 //
@@ -1281,8 +1290,28 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #ifdef TRAY_PROFILE_MATERIAL  // counts only (global atomics: its timings are not used)
     unsigned long long* prof_mat = p.stats + 32 + 2 * gridDim.x * (blockDim.x / 64u);
 #endif
+#ifdef TRAY_PROFILE_TIMELINE
+    unsigned long long* tl =
+        p.stats + 32 + (size_t)(blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * kTlStride;
+    const uint64_t tl_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t tl_prev = tl_start, tl_acc = 0;
+    uint32_t tl_busy = 0, tl_bucket = 0, tl_chunks = 0, tl_dry = 0;
+#endif
 
     while (true) {
+#ifdef TRAY_PROFILE_TIMELINE
+        {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            const uint32_t b = min((uint32_t)((tl_prev - tl_start) / kTlTicks), kTlBuckets - 1u);
+            if (b != tl_bucket) {
+                if (lane == 0) tl[4 + tl_bucket] = tl_acc;
+                tl_bucket = b;
+                tl_acc = 0;
+            }
+            tl_acc += (now - tl_prev) * tl_busy;
+            tl_prev = now;
+        }
+#endif
 #ifndef TRAY_PROFILE_REFILL  // slots 10, 13-15 hold the refill split instead
         PROF_CNT(10, 1);
 #endif
@@ -1327,8 +1356,14 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     c = take_chunk(p, uni, lane, grp_end >= p.late_at ? 1u : p.wave_chunks, cnt);
                     if (c == kPoolDone) {
                         exhausted = true;
+#ifdef TRAY_PROFILE_TIMELINE
+                        tl_dry = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tl_start);
+#endif
                         break;
                     }
+#ifdef TRAY_PROFILE_TIMELINE
+                    tl_chunks += cnt;
+#endif
                     grp_next = c + 1;
                     grp_end = c + cnt;
                 }
@@ -1480,6 +1515,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #endif
         PROF_ADD(0);
         TRAY_MARK("refill_end")
+#ifdef TRAY_PROFILE_TIMELINE
+        tl_busy = (uint32_t)__popcll(__ballot(L.busy));
+#endif
         if (__ballot(L.busy) == 0ull) {
             if (exhausted) break;
             continue;              // every lane drew a padding item: draw again
@@ -1640,6 +1678,17 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         atomicAdd(p.stats + 10, (unsigned long long)st.leaves);
 #endif
     }
+#ifdef TRAY_PROFILE_TIMELINE
+    if (kStats && lane == 0) {
+        const uint64_t end = __builtin_amdgcn_s_memrealtime();
+        tl_acc += (end - tl_prev) * tl_busy;
+        tl[4 + tl_bucket] = tl_acc;
+        tl[0] = tl_start;
+        tl[1] = end;
+        tl[2] = tl_dry;
+        tl[3] = tl_chunks;
+    }
+#endif
 #ifdef TRAY_PROFILE
     if (kStats && lane == 0) {
         for (int i = 0; i < 16; ++i) atomicAdd(p.stats + 3 + i, (unsigned long long)prof[i]);
