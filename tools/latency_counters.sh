@@ -2,7 +2,7 @@
 # Latency counters of the C2 megakernel (16-frame launches): LDS, instruction fetch, VMEM, SMEM
 # (rocprofv3 derived metrics: accumulated in-flight level / instruction count), one pass each pair.
 set -u
-O=gpurun_out/r9b; mkdir -p $O
+O=gpurun_out/lat; mkdir -p $O
 export TMPDIR=/tmp
 ARGS="--steps 16 --warmup 0 --no-cpu-baseline --no-e2e --no-single --frames-in-flight 1"
 i=0
