@@ -22,7 +22,8 @@
  *   "primary_candidates"  0: camera rays traverse the BVH instead of their
  *                         pixel's candidate list (same bits)
  *   "resolve_staged"      0: the plain per-pixel resolve instead of the LDS-staged
- *                         one for the ordered sum (same bits)
+ *                         one for the per-sample buffer (the ordered FP64 sum, and
+ *                         the fixed-point sums without on-chip slots) (same bits)
  *   "wave_chunks"         chunks a wave reserves per work-queue take (1..64), for
  *                         the whole launch (default: the build's size, single
  *                         chunks near the end of the queue) (same bits)

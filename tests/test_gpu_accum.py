@@ -34,11 +34,12 @@ def test_on_chip_equals_sample_buffer_and_oracle(L, O, scene, spp):
     st = camera(L, RICH_SETUP, w, h)
     base, bseg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 5)
     # per-sample buffer with integer resolve; one and two slots per wave (lanes wait for a free slot)
-    for slots in (0, 1, 2, 9):
-        with L.debug_knobs(acc_slots=slots):
+    # (slots 0: the LDS-staged integer resolve when 8 | r, and with resolve_staged=0 the plain one)
+    for slots, staged in ((0, 1), (0, 0), (1, 1), (2, 1), (9, 1)):
+        with L.debug_knobs(acc_slots=slots, resolve_staged=staged):
             rgb, seg = gpu_render(L, sc, DEFAULT_BG, st, w, h, spp, 50, 0.5, 5)
-        assert np.array_equal(seg, bseg), slots
-        assert np.array_equal(rgb, base), slots
+        assert np.array_equal(seg, bseg), (slots, staged)
+        assert np.array_equal(rgb, base), (slots, staged)
     ref, rseg = O.render(sc, DEFAULT_BG, st.as_array(), w, h, spp, 50, 0.5, 5, workers=WORKERS)
     check(base, bseg, ref, rseg)
 

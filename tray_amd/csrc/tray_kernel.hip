@@ -737,6 +737,14 @@ __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni
             const uint32_t pool_chunks = __builtin_amdgcn_readfirstlane(uni->pool_chunks);
             if (lane == 0) base = atomicAdd(p.queue, pool_chunks);
             base = __builtin_amdgcn_readlane(base, 0);
+#ifdef TRAY_GUIDED_POOL
+            {  // the next refill's size from what this one left in the queue (guided self-scheduling)
+                const uint32_t after = base + pool_chunks;
+                const uint32_t left = after < p.nchunks ? p.nchunks - after : 0u;
+                const uint32_t want = max(1u, min(p.pool_chunks, left / (gridDim.x * (uint32_t)TRAY_GUIDED_POOL)));
+                if (lane == 0) ((volatile __attribute__((address_space(3))) Uniforms*)uni)->pool_chunks = want;
+            }
+#endif
             const uint64_t fresh = base >= p.nchunks
                                        ? (uint64_t)kPoolDone << 32
                                        : ((uint64_t)min(base + pool_chunks, p.nchunks) << 32) | base;
@@ -1740,11 +1748,13 @@ constexpr int kStageStride = 25;  // doubles per pixel slab in LDS: 24 + 1 of pa
 
 // kMode: 0 FP64 sum in sample order, 1 the same staged through LDS (8 | r),
 // 2 fixed-point sums of the per-sample buffer, 3 fixed-point sums of the chunk
-// partials (on-chip accumulation, 64 | r).
-enum : int { kResolveF64 = 0, kResolveStaged = 1, kResolveFixed = 2, kResolvePartials = 3 };
+// partials (on-chip accumulation, 64 | r), 4 the fixed-point sums of 2 staged
+// through LDS like 1 (8 | r: r = 16, 32 renders without on-chip slots).
+enum : int { kResolveF64 = 0, kResolveStaged = 1, kResolveFixed = 2, kResolvePartials = 3, kResolveFixedStaged = 4 };
 template <int kFmt, int kMode>
 __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
-    constexpr bool kStaged = kMode == kResolveStaged;
+    constexpr bool kStaged = kMode == kResolveStaged || kMode == kResolveFixedStaged;
+    constexpr bool kFixedStaged = kMode == kResolveFixedStaged;
     __shared__ double srgb[256];
     if constexpr (kFmt == kOutRGBA8) {  // the encoder table, one entry per thread
         srgb[threadIdx.x] = p.srgb[threadIdx.x];
@@ -1787,6 +1797,8 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
         double* st = stage[threadIdx.x >> 6];
         const uint32_t q0 = q - lane;  // the wave's first pixel
         const double* base = p.samples + ((size_t)q0 * pix_stride + (size_t)blockIdx.y * (uint32_t)p.spp) * 3;
+        int64_t si[3] = {0, 0, 0};  // kFixedStaged: the pixel's integer totals
+        uint32_t bad = 0u;
         for (int32_t s = 0; s < p.spp; s += 8) {
 #pragma unroll
             for (int k = 0; k < 12; ++k) {  // 768 16-B pieces: pixel t / 12, piece t % 12 of its 192-B slab
@@ -1800,11 +1812,20 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double* mine = st + lane * kStageStride;
+            if constexpr (kFixedStaged) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) sum = add(sum, d3(mine[3 * k], mine[3 * k + 1], mine[3 * k + 2]));
+                for (int k = 0; k < 24; ++k) acc_add(__builtin_rint(mine[k]), 0x1p47, si[k % 3], bad, k % 3);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) sum = add(sum, d3(mine[3 * k], mine[3 * k + 1], mine[3 * k + 2]));
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();  // every lane has read the slab before it is overwritten
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if constexpr (kFixedStaged) {
+            if (valid) write_acc_mean<kFmt>(p, srgb, si, bad, x, j, pass);
+            return;
         }
     } else {
         if (!valid) return;
@@ -2035,11 +2056,13 @@ static KernelFn pick_resolve2(int fmt) {
 
 // The staged resolve needs 8 | rays per pixel (whole 8-sample slabs).
 static KernelFn pick_resolve(const KernelParams& p) {
-    if (p.acc_shift > 0)
-        return p.acc_slots > 0 ? pick_resolve2<kResolvePartials>(p.out_format) : pick_resolve2<kResolveFixed>(p.out_format);
     bool staged = p.spp % 8 == 0;
     long long v = 1;
     if (debug_knob(kKnobResolveStaged, &v)) staged = staged && v != 0;  // A/B
+    if (p.acc_shift > 0) {
+        if (p.acc_slots > 0) return pick_resolve2<kResolvePartials>(p.out_format);
+        return staged ? pick_resolve2<kResolveFixedStaged>(p.out_format) : pick_resolve2<kResolveFixed>(p.out_format);
+    }
     return staged ? pick_resolve2<kResolveStaged>(p.out_format) : pick_resolve2<kResolveF64>(p.out_format);
 }
 
