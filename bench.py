@@ -67,6 +67,10 @@ Also reported (rank 0):
                C3/C5): the FP64 output (tray_render_async, TRAY_OUT_RGB_F64) and
                frame 0 of a passes launch in the timed shape (TRAY_OUT_RGB_F32),
                plus the per-pixel Scene.Hit counts (bit-exact). Gate 1e-4.
+               At N > 1 the same check runs on the frame rank 0 ASSEMBLES: every
+               rank renders pass 0 of its rows again (untimed), the timed run's
+               gather brings the row tiles to rank 0, and the oracle renders the
+               same rows there (gather_pass0, gathered_parity).
   ranks        (N > 1) each rank's render time per frame (HIP events, one
                launch of F frames of its rows) and one gather of F frames, so
                a measured curve separates imbalance from the gather.
@@ -189,23 +193,31 @@ def launch_ranks(n: int, argv: list, timeout: float | None = None, script: str |
     return rc
 
 
-_PHASE = ["start"]
+_PHASE = ["start", time.monotonic()]
 
 
 def set_phase(name: str) -> None:
-    """What this rank is doing, for the watchdog's message."""
-    _PHASE[0] = name
+    """What this rank is doing, for the watchdog's message; re-arms the watchdog's
+    per-phase deadline (start_watchdog)."""
+    _PHASE[:] = [name, time.monotonic()]
 
 
 def start_watchdog(rank: int, seconds: float) -> None:
-    """A daemon thread that ends this rank (exit status 124) once it has run for
-    `seconds`, naming the rank and its phase: a collective that never completes
-    (a peer that died, an RCCL hang) then fails the job instead of holding it."""
+    """A daemon thread that ends this rank (exit status 124) once it has spent
+    `seconds` in ONE phase (set_phase re-arms the deadline), naming the rank and
+    the phase: a collective that never completes (a peer that died, an RCCL hang)
+    then fails the job instead of holding it, while a long but progressing run
+    (many --steps, a big config) is never cut off for its total length."""
     import threading
 
     def watch():
-        time.sleep(seconds)
-        print(f"bench.py: rank {rank} still running after {seconds} s (--rank-timeout), in phase "
+        while True:
+            name, t0 = _PHASE
+            left = t0 + seconds - time.monotonic()
+            if left <= 0:
+                break
+            time.sleep(min(left, 1.0))
+        print(f"bench.py: rank {rank} still running after {seconds} s (--rank-timeout) in phase "
               f"'{_PHASE[0]}': exiting", file=sys.stderr, flush=True)
         os._exit(124)
 
@@ -243,9 +255,10 @@ def main() -> int:
                     help="frames per launch, the same at every N (tray_render_passes_async: consecutive "
                          "progressive passes in one persistent launch, one tail of long paths per launch)")
     ap.add_argument("--rank-timeout", type=float, default=900.0,
-                    help="N > 1: a rank still running after this many seconds exits 124 naming its phase (under any "
-                         "launcher; also the process group's collective timeout), and bench.py's own launcher stops "
-                         "the ranks still running (0: no limit)")
+                    help="N > 1: a rank that spends this many seconds in one phase (scene upload, warmup, timed "
+                         "frames, ...) exits 124 naming it (under any launcher; also the process group's collective "
+                         "timeout); bench.py's own launcher stops every rank once one fails, and the ranks still "
+                         "running after 8x this long in total (0: no limit)")
     ap.add_argument("--cpu-min-seconds", type=float, default=10.0,
                     help="cpu_baseline: render further progressive passes of the sample until this much time has "
                          "passed (small frames, C1)")
@@ -254,7 +267,8 @@ def main() -> int:
         ap.error("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # No launcher: start the N ranks here, before anything touches the GPU.
-        return launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout if args.rank_timeout > 0 else None)
+        # The ranks' watchdogs bound each phase; this bounds the whole run as a backstop.
+        return launch_ranks(args.gpus, sys.argv[1:], 8 * args.rank_timeout if args.rank_timeout > 0 else None)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -180,3 +180,17 @@ def test_rank_watchdog_names_rank_and_phase():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert r.returncode == 124 and time.monotonic() - t0 < 30
     assert "rank 3 still running after 1.0 s" in r.stderr and "'timed frames'" in r.stderr
+
+
+def test_rank_watchdog_is_per_phase():
+    """The watchdog bounds each phase, not the run: a rank whose phases
+    each finish within the limit runs on past it in total and exits normally."""
+    import time
+
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; bench.start_watchdog(4, 1.5)\n"
+            "for k in range(4):\n    bench.set_phase('phase %%d' %% k); time.sleep(0.8)\n"
+            "print('done')" % ROOT)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "done", r.stderr
+    assert time.monotonic() - t0 > 3.0  # longer in total than the limit
