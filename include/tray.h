@@ -21,17 +21,22 @@
  * ray/materials.go, ray/camera.go). Division and sqrt are correctly rounded.
  *
  * Counter RNG contract (replaces fortio.org/rand v1.1.0, go.mod:9, which is not
- * vendored): every random draw comes from one Philox4x32-10 block (Salmon et al.
- * 2011, Random123 constants) with
- *     key = (seed & 0xffffffff, seed >> 32)
- *     ctr = (pixel, sample, bounce, purpose << 24)
+ * vendored). Philox4x32-10 (Salmon et al. 2011, Random123 constants), keyed by
+ * (seed & 0xffffffff, seed >> 32), gives
+ *     the draw key  (k0, k1, k2, k3) = Philox(ctr = (0, 0, 0, 5 << 24))
+ *     host scene generation: ctr = (draw_index, 0, 0, 4 << 24),
+ *                 Float64 = ((x1 << 32 | x0) >> 11) * 2^-53
+ * Every renderer draw comes from one DRAW BLOCK (ABI 6; ABI 5 used a Philox
+ * block here, ~7.6 % of the frame): pcg4d (Jarzynski & Olano, "Hash Functions
+ * for GPU Rendering", JCGT 9(3), 2020) of the keyed counter, then an xorshift:
+ *     v = (pixel ^ k0, sample ^ k1, bounce ^ k2, purpose ^ k3)
+ *     v = v * 1664525 + 1013904223                        (each word, mod 2^32)
+ *     twice: v0 += v1*v3; v1 += v2*v0; v2 += v0*v1; v3 += v1*v2; v ^= v >> 16
  *     pixel = y * width + x in GLOBAL image coordinates (tiling-independent)
  *     purpose 1 = the sample's camera block (bounce = 0): words 0,1 feed the
  *                 anti-aliasing disc (ray/tracer.go:138), words 2,3 the lens
  *                 disc (ray/camera.go:128)
  *     purpose 3 = the scatter block of hit number `bounce` (ray/materials.go:14,31,57)
- *     purpose 4 = host scene generation: ctr = (draw_index, 0, 0, 4 << 24),
- *                 Float64 = ((x1 << 32 | x0) >> 11) * 2^-53
  * Renderer uniforms are ui = xi * 2^-32 in [0,1). Samplers (no rejection loops):
  *     InDisc(r)   = (sqrt(ua) * cos(2 pi ub) * r, sqrt(ua) * sin(2 pi ub) * r)
  *     UnitVector  = z = 1 - 2 u0, s = sqrt(1 - z*z), (s cos(2 pi u1), s sin(2 pi u1), z)
@@ -59,9 +64,10 @@
 extern "C" {
 #endif
 
-#define TRAY_ABI_VERSION 5 /* 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get;
+#define TRAY_ABI_VERSION 6 /* 2: tray_render_devices_progress, tray_release_cache; 3: tray_render_plan_get;
                               4: TRAY_FLAG_ORDERED_SUM (the library no longer reads the process environment);
-                              5: a scene handle may be rendered on several streams at once (launch contexts) */
+                              5: a scene handle may be rendered on several streams at once (launch contexts);
+                              6: renderer draws from the keyed pcg4d draw block (other pixels than ABI 5) */
 
 typedef enum tray_status {
     TRAY_OK = 0,

@@ -61,6 +61,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_ray_color.argtypes = [_vp, ctypes.c_int, _dp, _dp, _dp, ctypes.c_int, ctypes.c_uint64,
                                        ctypes.c_uint32, ctypes.c_uint32, _dp, _u32p]
         L.oracle_philox4x32_10.argtypes = [_u32p, _u32p, _u32p]
+        L.oracle_draw_key.argtypes = [ctypes.c_uint64, _u32p]
+        L.oracle_draw_block.argtypes = [_u32p] + [ctypes.c_uint32] * 4 + [_u32p]
         L.oracle_uniforms.argtypes = [ctypes.c_uint64] + [ctypes.c_uint32] * 4 + [_dp]
         L.oracle_unit_vector.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _dp]
         L.oracle_in_disc.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -117,6 +119,21 @@ def philox4x32_10(ctr, key) -> tuple[int, int, int, int]:
     k = (ctypes.c_uint32 * 2)(*key)
     o = (ctypes.c_uint32 * 4)()
     lib().oracle_philox4x32_10(c, k, o)
+    return tuple(o)
+
+
+def draw_key(seed) -> tuple[int, int, int, int]:
+    """The renderer's draw key of a seed (include/tray.h, ABI 6)."""
+    o = (ctypes.c_uint32 * 4)()
+    lib().oracle_draw_key(seed, o)
+    return tuple(o)
+
+
+def draw_block(key, pixel, sample, bounce, purpose) -> tuple[int, int, int, int]:
+    """The renderer's draw block (include/tray.h, ABI 6): keyed pcg4d + xorshift-16."""
+    k = (ctypes.c_uint32 * 4)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().oracle_draw_block(k, pixel, sample, bounce, purpose, o)
     return tuple(o)
 
 

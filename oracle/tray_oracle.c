@@ -12,7 +12,7 @@
  * with one documented substitution: the random stream. fortio.org/rand v1.1.0
  * (go.mod:9) is not available, so every draw comes from the counter-based RNG
  * specified in include/tray.h ("Counter RNG contract"), keyed on
- * (seed, pixel, sample, bounce, purpose, attempt). The draw SCHEDULE (which
+ * (seed; pixel, sample, bounce, purpose). The draw SCHEDULE (which
  * call sites draw, and when) follows the reference.
  *
  * Parity pinning: the vector/material/camera math is
@@ -123,7 +123,8 @@ static inline vec3 refract(vec3 uv, vec3 n, double etai_over_etat) {
 static inline double pow5(double x) { double x2 = x * x; double x4 = x2 * x2; return x * x4; }
 
 /* ------------------------------------------------------------------ */
-/* Counter RNG (include/tray.h "Counter RNG contract"): Philox4x32-10. */
+/* Counter RNG (include/tray.h "Counter RNG contract"): Philox4x32-10 for the  */
+/* draw key and the host's scene stream, the keyed pcg4d draw block for draws. */
 /* ------------------------------------------------------------------ */
 #define PH_M0 0xD2511F53u
 #define PH_M1 0xCD9E8D57u
@@ -146,14 +147,38 @@ static void philox4x32_10(const uint32_t in[4], const uint32_t key[2], uint32_t 
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-enum { P_CAMERA = 1, P_SCATTER = 3, P_SCENE = 4 };
+enum { P_CAMERA = 1, P_SCATTER = 3, P_SCENE = 4, P_KEY = 5 };
 
-/* One Philox block as four 32-bit uniforms u = x * 2^-32 in [0,1). */
-static void uniforms4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, double u[4]) {
-    uint32_t ctr[4] = {c0, c1, c2, c3};
+/* The renderer's draw key (include/tray.h, ABI 6): Philox4x32-10 of the seed at
+ * ctr = (0, 0, 0, P_KEY << 24). */
+static void draw_key(uint64_t seed, uint32_t k[4]) {
+    uint32_t ctr[4] = {0u, 0u, 0u, (uint32_t)P_KEY << 24};
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    philox4x32_10(ctr, key, k);
+}
+
+/* The renderer's draw block (include/tray.h, ABI 6): pcg4d (Jarzynski & Olano,
+ * JCGT 9(3) 2020) of the keyed counter, then v ^= v >> 16 on each word. All
+ * arithmetic mod 2^32. */
+static void draw_block(const uint32_t k[4], uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t purpose,
+                       uint32_t out[4]) {
+    uint32_t v[4] = {pixel ^ k[0], sample ^ k[1], bounce ^ k[2], purpose ^ k[3]};
+    for (int i = 0; i < 4; ++i) v[i] = v[i] * 1664525u + 1013904223u;
+    for (int round = 0; round < 2; ++round) {
+        v[0] += v[1] * v[3];
+        v[1] += v[2] * v[0];
+        v[2] += v[0] * v[1];
+        v[3] += v[1] * v[2];
+        for (int i = 0; i < 4; ++i) v[i] ^= v[i] >> 16;
+    }
+    for (int i = 0; i < 4; ++i) out[i] = v[i];
+}
+
+/* One draw block as four 32-bit uniforms u = x * 2^-32 in [0,1). */
+static void uniforms4(const uint32_t key[4], uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t purpose,
+                      double u[4]) {
     uint32_t x[4];
-    philox4x32_10(ctr, key, x);
+    draw_block(key, pixel, sample, bounce, purpose, x);
     for (int i = 0; i < 4; ++i) u[i] = (double)x[i] * 0x1.0p-32;
 }
 
@@ -210,14 +235,23 @@ static void sincos_2pi(double u, double *s, double *c) {
     }
 }
 
-typedef struct { uint64_t seed; uint32_t pixel; uint32_t sample; } rngkey;
+/* A sample's draws: the render's draw key (computed once per render) and the
+ * sample's counter words. */
+typedef struct { uint32_t key[4]; uint32_t pixel; uint32_t sample; } rngkey;
+static rngkey make_rngkey(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    rngkey k;
+    draw_key(seed, k.key);
+    k.pixel = pixel;
+    k.sample = sample;
+    return k;
+}
 
 /* InDisc(radius) replacement (ray/tracer.go:138, ray/camera.go:128): polar map
  * of two uniforms of the sample's camera block; which = 0 (anti-aliasing,
  * words 0,1) or 1 (lens, words 2,3). */
 static void in_disc(rngkey k, int which, double radius, double *ox, double *oy) {
     double u[4];
-    uniforms4(k.seed, k.pixel, k.sample, 0u, (uint32_t)P_CAMERA << 24, u);
+    uniforms4(k.key, k.pixel, k.sample, 0u, (uint32_t)P_CAMERA, u);
     double r = sqrt(u[2 * which]);
     double s, c;
     sincos_2pi(u[2 * which + 1], &s, &c);
@@ -230,7 +264,7 @@ static void in_disc(rngkey k, int which, double radius, double *ox, double *oy) 
  * scatter block. */
 static vec3 random_unit_vector(rngkey k, uint32_t bounce) {
     double u[4];
-    uniforms4(k.seed, k.pixel, k.sample, bounce, (uint32_t)P_SCATTER << 24, u);
+    uniforms4(k.key, k.pixel, k.sample, bounce, (uint32_t)P_SCATTER, u);
     double z = 1.0 - 2.0 * u[0];
     double r = sqrt(1.0 - z * z);
     double s, c;
@@ -242,7 +276,7 @@ static vec3 random_unit_vector(rngkey k, uint32_t bounce) {
  * bounce's scatter block. */
 static double random_float64(rngkey k, uint32_t bounce) {
     double u[4];
-    uniforms4(k.seed, k.pixel, k.sample, bounce, (uint32_t)P_SCATTER << 24, u);
+    uniforms4(k.key, k.pixel, k.sample, bounce, (uint32_t)P_SCATTER, u);
     return u[0];
 }
 
@@ -425,6 +459,7 @@ typedef struct {
     double ray_radius;
     uint64_t seed;
     uint32_t sample_base; /* progressive pass x spp (tray_params.pass, include/tray.h) */
+    uint32_t key[4];      /* the draw key of the seed (draw_key) */
 } o_params;
 
 /* One pixel of Tracer.RenderLines ray/tracer.go:129-145 (linear mean colour). */
@@ -436,7 +471,8 @@ static int render_pixel(const scene *sc, const o_camera *cam, const o_params *p,
     uint32_t segs = 0;
     int err = 0;
     for (int s = 0; s < p->spp; ++s) {
-        rngkey k = {p->seed, (uint32_t)y * (uint32_t)p->width + (uint32_t)x, p->sample_base + (uint32_t)s};
+        rngkey k = {{p->key[0], p->key[1], p->key[2], p->key[3]}, (uint32_t)y * (uint32_t)p->width + (uint32_t)x,
+                    p->sample_base + (uint32_t)s};
         double ox = 0.0, oy = 0.0;
         if (multiple_rays) in_disc(k, 0, p->ray_radius, &ox, &oy);
         ray r = get_ray(cam, k, (double)x, (double)y, ox, oy);
@@ -512,7 +548,8 @@ ORACLE_EXPORT int oracle_render_rows(const o_sphere *spheres, int n, const doubl
         if (rows[i] < 0 || rows[i] >= height) return -1;
     scene sc = {spheres, n, V(bg[0], bg[1], bg[2]), V(bg[3], bg[4], bg[5])};
     if (pass < 0) return -1;
-    o_params p = {width, height, spp, max_depth, ray_radius, seed, (uint32_t)pass * (uint32_t)spp};
+    o_params p = {width, height, spp, max_depth, ray_radius, seed, (uint32_t)pass * (uint32_t)spp, {0, 0, 0, 0}};
+    draw_key(seed, p.key);
     job j = {&sc, cam, &p, rows, nrows, 0, out_rgb, out_segments, 0, 0};
     if (workers <= 1) {
         render_row_range(&j, 0, nrows);
@@ -535,7 +572,8 @@ ORACLE_EXPORT int oracle_render_pixels(const o_sphere *spheres, int n, const dou
     if (width <= 0 || height <= 0 || spp <= 0 || max_depth <= 0 || pass < 0) return -1;
     if (!valid_scene(spheres, n)) return -2;
     scene sc = {spheres, n, V(bg[0], bg[1], bg[2]), V(bg[3], bg[4], bg[5])};
-    o_params p = {width, height, spp, max_depth, ray_radius, seed, (uint32_t)pass * (uint32_t)spp};
+    o_params p = {width, height, spp, max_depth, ray_radius, seed, (uint32_t)pass * (uint32_t)spp, {0, 0, 0, 0}};
+    draw_key(seed, p.key);
     for (int i = 0; i < count; ++i) {
         uint32_t s = 0;
         if (xs[i] < 0 || xs[i] >= width || ys[i] < 0 || ys[i] >= height) return -1;
@@ -551,7 +589,7 @@ ORACLE_EXPORT int oracle_ray_color(const o_sphere *spheres, int n, const double 
                                    double out[3], uint32_t *segments) {
     scene sc = {spheres, n, V(bg[0], bg[1], bg[2]), V(bg[3], bg[4], bg[5])};
     ray r = {V(origin[0], origin[1], origin[2]), V(dir[0], dir[1], dir[2])};
-    rngkey k = {seed, pixel, sample};
+    rngkey k = make_rngkey(seed, pixel, sample);
     uint32_t segs = 0;
     int err = 0;
     vec3 c = ray_color(&sc, &r, depth, k, 0u, &segs, &err);
@@ -566,19 +604,24 @@ ORACLE_EXPORT int oracle_ray_color(const o_sphere *spheres, int n, const double 
 ORACLE_EXPORT void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
     philox4x32_10(ctr, key, out);
 }
+ORACLE_EXPORT void oracle_draw_key(uint64_t seed, uint32_t out[4]) { draw_key(seed, out); }
+ORACLE_EXPORT void oracle_draw_block(const uint32_t key[4], uint32_t pixel, uint32_t sample, uint32_t bounce,
+                                     uint32_t purpose, uint32_t out[4]) {
+    draw_block(key, pixel, sample, bounce, purpose, out);
+}
 ORACLE_EXPORT void oracle_uniforms(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                    double out[2]) {
     uniforms2(seed, c0, c1, c2, c3, out);
 }
 ORACLE_EXPORT void oracle_unit_vector(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
                                       double out[3]) {
-    rngkey k = {seed, pixel, sample};
+    rngkey k = make_rngkey(seed, pixel, sample);
     vec3 v = random_unit_vector(k, bounce);
     out[0] = v.x; out[1] = v.y; out[2] = v.z;
 }
 ORACLE_EXPORT void oracle_in_disc(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t which, double radius,
                                   double out[2]) {
-    rngkey k = {seed, pixel, sample};
+    rngkey k = make_rngkey(seed, pixel, sample);
     in_disc(k, (int)which, radius, &out[0], &out[1]);
 }
 ORACLE_EXPORT void oracle_sincos_2pi(double u, double out[2]) { sincos_2pi(u, &out[0], &out[1]); }
@@ -601,7 +644,7 @@ ORACLE_EXPORT void oracle_unit(const double v[3], double out[3]) {
  * lens draw (if Aperture > 0) is keyed on (seed, pixel, sample). */
 ORACLE_EXPORT void oracle_get_ray(const o_camera *cam, uint64_t seed, uint32_t pixel, uint32_t sample, double px,
                                   double py, double ox, double oy, double origin[3], double dir[3]) {
-    rngkey k = {seed, pixel, sample};
+    rngkey k = make_rngkey(seed, pixel, sample);
     ray r = get_ray(cam, k, px, py, ox, oy);
     origin[0] = r.origin.x; origin[1] = r.origin.y; origin[2] = r.origin.z;
     dir[0] = r.dir.x; dir[1] = r.dir.y; dir[2] = r.dir.z;
@@ -648,7 +691,7 @@ ORACLE_EXPORT int oracle_scatter(const o_sphere *s, const double in_origin[3], c
     hr.t = 0;
     hr.mat = 0;
     hr.front_face = front_face;
-    rngkey k = {seed, pixel, sample};
+    rngkey k = make_rngkey(seed, pixel, sample);
     vec3 a;
     ray out;
     int res = scatter(&sc, &r, &hr, k, bounce, &a, &out);

@@ -19,7 +19,7 @@ def test_exports_match_header(L):
     lib = L.lib()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.tray_abi_version() == 5  # 2: devices_progress, release_cache; 3: plan_get; 4: ORDERED_SUM flag; 5: launch contexts
+    assert lib.tray_abi_version() == 6  # 2: devices_progress, release_cache; 3: plan_get; 4: ORDERED_SUM flag; 5: launch contexts; 6: pcg4d draws
 
 
 def test_debug_hooks_outside_stable_header(L):

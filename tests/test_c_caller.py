@@ -27,7 +27,7 @@ def _run_caller(tmp_path):
 
 
 def _check_host_side(out):
-    assert out["abi"] == "5" and out["spheres"] == "486" and out["rows"] == "9"
+    assert out["abi"] == "6" and out["spheres"] == "486" and out["rows"] == "9"
     assert out["focus"] == "10"
     assert out["srgb"] == "0,188,255,10,0,255"  # ray/vec3_test.go:264-289: 0, 0.5 -> 188, 1, clamps
     assert out["bad_width"] == "-1" and out["bad_reserved"] == "-1"  # TRAY_ERR_INVALID_ARGUMENT

@@ -47,12 +47,12 @@ def test_sincos_2pi(O):
 
 
 def test_camera_block_shared(O):
-    """AA (words 0,1) and lens (words 2,3) discs come from one Philox block per sample."""
+    """AA (words 0,1) and lens (words 2,3) discs come from one draw block per sample
+    (purpose 1, include/tray.h)."""
     a = O.in_disc(5, 77, 3, 0, 1.0)
     b = O.in_disc(5, 77, 3, 1, 1.0)
     assert tuple(a) != tuple(b)
-    ctr = (77, 3, 0, 1 << 24)
-    x = O.philox4x32_10(ctr, (5, 0))
+    x = O.draw_block(O.draw_key(5), 77, 3, 0, 1)
     u = [v * 2.0**-32 for v in x]
     s, c = O.sincos_2pi(u[1])
     assert tuple(a) == ((u[0] ** 0.5 * c) * 1.0, (u[0] ** 0.5 * s) * 1.0)

@@ -16,8 +16,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-BUCKETS, TICKS = 1024, 1000  # kTlBuckets, kTlTicks (100 MHz clock: 10 us)
-STRIDE = BUCKETS + 4
+BUCKETS, MT_TICKS, HDR = 1024, 25000, 6  # kTlBuckets, kTlTicks (shader clock), kTlHdr
+TICKS = 1000  # output buckets: 10 us of the 100 MHz constant clock
+STRIDE = BUCKETS + HDR
 
 
 def main():
@@ -55,17 +56,20 @@ def main():
     rec = stats[32:].view(args.waves, STRIDE).cpu().numpy().astype(np.float64)
     seen = rec[:, 1] > 0
     rec = rec[seen]
+    last = rec[:, HDR + BUCKETS - 3:HDR + BUCKETS].astype(np.int64)  # last path: segments, pixel, sample
+    rec[:, HDR + BUCKETS - 3:] = 0
     start, end, dry, chunks = rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3]
+    ratio = (end - start) / np.maximum(rec[:, 5] - rec[:, 4], 1)  # constant-clock ticks per shader tick
     g0 = start.min()
     span = end.max() - g0
     lanes = 64 * len(rec)
     nb = int(span // TICKS) + 2
     curve = np.zeros(nb)
     for w in range(len(rec)):
-        off = int((start[w] - g0) // TICKS)
-        b = rec[w, 4:]
-        n = min(BUCKETS, nb - off)
-        curve[off:off + n] += b[:n]
+        b = rec[w, HDR:HDR + BUCKETS - 3] * ratio[w]  # busy lane x constant-clock ticks
+        mid = start[w] - g0 + (np.arange(b.size) + 0.5) * MT_TICKS * ratio[w]
+        idx = np.minimum((mid // TICKS).astype(np.int64), nb - 1)
+        np.add.at(curve, idx, b)
     util = curve / (TICKS * lanes)  # busy-lane fraction of the whole grid per bucket
     dry_abs = start + dry - g0
     has_dry = dry > 0
@@ -75,7 +79,7 @@ def main():
     t_first = int(first_dry // TICKS)
     q = [0, 1, 10, 50, 90, 99, 100]
     d = {
-        "config": args.config, "shard": args.shard, "waves": int(len(rec)), "span_us": round(span / 100, 1),
+        "config": args.config, "shard": args.shard, "shader_ghz": round(float(np.median(100e6 / ratio)) / 1e9, 3), "waves": int(len(rec)), "span_us": round(span / 100, 1),
         "lane_util_overall": round(busy_total / (span * lanes), 4),
         "first_dry_us": round(first_dry / 100, 1), "last_dry_us": round(last_dry / 100, 1),
         "end_us_pct": {str(k): round(float(np.percentile(end_rel, k)) / 100, 1) for k in q},
@@ -87,6 +91,15 @@ def main():
         "util_first_100us": round(float(util[:10].mean()), 4),
         "util_steady": round(float(util[10:max(11, t_first)].mean()), 4),
     }
+    # what the last waves trace: the wave's final lone path (segments so far, pixel, sample)
+    order = np.argsort(end_rel)[::-1][:32]
+    d["last_waves"] = [{"end_us": round(float(end_rel[w]) / 100, 1), "drain_us": round(float(end[w] - start[w] - dry[w]) / 100, 1),
+                        "segments": int(last[w, 0]), "x": int(last[w, 1] % W), "y": int(last[w, 1] // W),
+                        "sample": int(last[w, 2])} for w in order]
+    seg_all = last[:, 0][last[:, 0] > 0]
+    d["last_path_segments_pct"] = {str(k): float(np.percentile(seg_all, k)) for k in q} if seg_all.size else None
+    drain = (end - start - dry)[has_dry] / 100
+    d["wave_drain_us_pct"] = {str(k): round(float(np.percentile(drain, k)), 1) for k in q}
     if args.curve:
         d["util_curve"] = [round(float(u), 3) for u in util]
     print(json.dumps(d), flush=True)

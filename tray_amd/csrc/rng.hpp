@@ -1,10 +1,11 @@
 // Counter RNG of the tray C-ABI (include/tray.h, "Counter RNG contract").
 //
 // Replaces fortio.org/rand v1.1.0 (go.mod:9), whose per-row-chunk sequential
-// stream (ray/tracer.go:121) cannot be reproduced here. Philox4x32-10 keyed on
-// (seed) with counter (pixel, sample, bounce, purpose<<24 | attempt) makes every
-// draw a pure function of where it happens, so a pixel's colour does not depend
-// on launch geometry, row tiling or device count.
+// stream (ray/tracer.go:121) cannot be reproduced here. Every renderer draw is a
+// pure function of where it happens - (seed; pixel, sample, bounce, purpose) -
+// so a pixel's colour does not depend on launch geometry, row tiling or device
+// count. ABI 6: the draws come from draw_block (a keyed pcg4d hash, below), the
+// key and the host's scene generation from Philox4x32-10.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -12,7 +13,7 @@
 
 namespace tray {
 
-enum : uint32_t { kPurposeCamera = 1, kPurposeScatter = 3, kPurposeScene = 4 };
+enum : uint32_t { kPurposeCamera = 1, kPurposeScatter = 3, kPurposeScene = 4, kPurposeKey = 5 };
 
 struct U2 {
     double u0, u1;
@@ -25,8 +26,9 @@ struct Block {
     uint32_t x0, x1, x2, x3;
 };
 
-// Philox4x32-10 (Salmon et al. 2011, Random123 constants). TRAY_PHILOX_ROUNDS
-// exists only for cost experiments (tools/build_variants.sh); the contract is 10.
+// Philox4x32-10 (Salmon et al. 2011, Random123 constants): the draw key and the
+// host's scene stream. TRAY_PHILOX_ROUNDS exists only for cost experiments
+// (tools/build_variants.sh); the contract is 10.
 #ifndef TRAY_PHILOX_ROUNDS
 #define TRAY_PHILOX_ROUNDS 10
 #endif
@@ -51,6 +53,46 @@ __host__ __device__ __forceinline__ Block philox4x32_10(uint64_t seed, uint32_t 
     return Block{c0, c1, c2, c3};
 }
 
+// The renderer's draw key (include/tray.h, ABI 6): one Philox4x32-10 block of the
+// seed, ctr = (0, 0, 0, kPurposeKey << 24), computed once per render on the host.
+struct DrawKey {
+    uint32_t k0, k1, k2, k3;
+};
+__host__ __device__ inline DrawKey draw_key(uint64_t seed) {
+    const Block b = philox4x32_10(seed, 0u, 0u, 0u, kPurposeKey << 24);
+    return DrawKey{b.x0, b.x1, b.x2, b.x3};
+}
+
+// The renderer's draw block (include/tray.h, ABI 6): pcg4d (Jarzynski & Olano,
+// "Hash Functions for GPU Rendering", JCGT 9(3), 2020) of the keyed counter
+// (pixel ^ k0, sample ^ k1, bounce ^ k2, purpose ^ k3), then an xorshift-16 of
+// each word. The xorshift mixes the low output bits (a product's low bits depend
+// only on its factors' low bits; without it flipping counter bit 17 never flips
+// output bit 0), and the Philox key spreads nearby seeds. Twelve 32-bit products
+// where Philox4x32-10 needs twenty 32x32 -> 64-bit ones and 40 XORs: a Philox
+// block was ~7.6 % of the C2 frame (rounds 10 / 7 / 4: 78.06 / 76.33 / 74.44 ms
+// per 16-frame launch, profiles/r10_ab_rng_c2.jsonl). Strict avalanche over the
+// counter bits the renderer varies, bit bias and word correlations are at noise
+// level (tests/test_rng_quality_cpu.py).
+__host__ __device__ __forceinline__ Block draw_block(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint32_t pixel,
+                                                     uint32_t sample, uint32_t bounce, uint32_t purpose) {
+    uint32_t v0 = (pixel ^ k0) * 1664525u + 1013904223u, v1 = (sample ^ k1) * 1664525u + 1013904223u;
+    uint32_t v2 = (bounce ^ k2) * 1664525u + 1013904223u, v3 = (purpose ^ k3) * 1664525u + 1013904223u;
+    v0 += v1 * v3;
+    v1 += v2 * v0;
+    v2 += v0 * v1;
+    v3 += v1 * v2;
+    v0 ^= v0 >> 16;
+    v1 ^= v1 >> 16;
+    v2 ^= v2 >> 16;
+    v3 ^= v3 >> 16;
+    v0 += v1 * v3;
+    v1 += v2 * v0;
+    v2 += v0 * v1;
+    v3 += v1 * v2;
+    return Block{v0 ^ (v0 >> 16), v1 ^ (v1 >> 16), v2 ^ (v2 >> 16), v3 ^ (v3 >> 16)};
+}
+
 // One block -> two 53-bit uniforms in [0,1) (host scene generation).
 __host__ __device__ __forceinline__ U2 philox_uniforms(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2,
                                                        uint32_t c3) {
@@ -61,13 +103,6 @@ __host__ __device__ __forceinline__ U2 philox_uniforms(uint64_t seed, uint32_t c
     u.u0 = (double)(a >> 11) * 0x1.0p-53;
     u.u1 = (double)(c >> 11) * 0x1.0p-53;
     return u;
-}
-
-// One block -> four 32-bit uniforms u = x * 2^-32 in [0,1) (renderer draws).
-__host__ __device__ __forceinline__ U4 philox_u4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-    const Block b = philox4x32_10(seed, c0, c1, c2, c3);
-    return U4{(double)b.x0 * 0x1.0p-32, (double)b.x1 * 0x1.0p-32, (double)b.x2 * 0x1.0p-32,
-              (double)b.x3 * 0x1.0p-32};
 }
 
 // sin and cos of 2*pi*u, u in [0,1) (the "sincos2pi" of include/tray.h). The

@@ -23,6 +23,7 @@
 #include "../../include/tray_debug.h"
 #include "tray_internal.hpp"
 #include "bvh.hpp"
+#include "rng.hpp"
 #include "tray_kernel.hpp"
 
 namespace tray {
@@ -580,7 +581,10 @@ static int prepare_render(tray_scene_t sc, const tray_camera* cam, const tray_pa
     k.out_format = p->output;
     k.ray_radius = p->ray_radius;
     k.focus_time = cam->focus_distance / cam->focal_length;  // ray/camera.go:134
-    k.seed = p->seed;
+    {
+        const DrawKey dk = draw_key(p->seed);  // include/tray.h, ABI 6
+        k.key[0] = dk.k0, k.key[1] = dk.k1, k.key[2] = dk.k2, k.key[3] = dk.k3;
+    }
     memcpy(k.cam.position, cam->position, sizeof(k.cam.position));
     memcpy(k.cam.pixel00, cam->pixel00, sizeof(k.cam.pixel00));
     memcpy(k.cam.pixel_x, cam->pixel_x, sizeof(k.cam.pixel_x));

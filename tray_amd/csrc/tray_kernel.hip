@@ -133,7 +133,7 @@ __device__ __forceinline__ double reflectance(double cosine, double r0) {
     return r0 + (1 - r0) * (x * x4);
 }
 
-// The uniform u = w 2^-32 of a 32-bit Philox word (include/tray.h).
+// The uniform u = w 2^-32 of a 32-bit word of a draw block (include/tray.h).
 __device__ __forceinline__ double uniform(uint32_t w) { return (double)w * 0x1.0p-32; }
 
 // InDisc(radius) (ray/tracer.go:138, ray/camera.go:128): polar map of two
@@ -157,7 +157,7 @@ struct Uniforms {
     CamRec cam;
     V3 bg_a, bg_b;
     double focus_time, ray_radius;
-    uint64_t seed;
+    uint32_t key[4];  // the draw key (rng.hpp draw_key of the seed)
     uint64_t pool;  // the workgroup's chunk pool: (end << 32) | next (take_chunk)
     uint32_t pool_chunks;  // chunks per pool refill (read only when refilling)
 };
@@ -165,14 +165,15 @@ struct Uniforms {
 // (slow, system-coherent) flat loads.
 typedef const volatile __attribute__((address_space(3))) Uniforms* UniPtr;
 
-// The RNG key, re-read per draw and made wave-uniform: Philox's round keys are
-// then recomputed with scalar adds instead of being hoisted out of the loop
-// (where they would be spilled to VGPR lanes and cost a v_readlane each).
-__device__ __forceinline__ uint64_t uni_seed(UniPtr uni) {
-    const uint64_t s = uni->seed;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)s);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(s >> 32));
-    return ((uint64_t)hi << 32) | lo;
+// A word of the draw key, re-read per draw and made wave-uniform (a scalar
+// operand of the hash's XORs) instead of being hoisted out of the loop, where it
+// would be spilled to a VGPR lane and cost a v_readlane on every use.
+__device__ __forceinline__ uint32_t uni_key(UniPtr uni, int i) { return __builtin_amdgcn_readfirstlane(uni->key[i]); }
+
+// The draw block of (pixel, sample, bounce, purpose) (include/tray.h, rng.hpp draw_block).
+__device__ __forceinline__ Block draw(UniPtr uni, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t purpose) {
+    return draw_block(uni_key(uni, 0), uni_key(uni, 1), uni_key(uni, 2), uni_key(uni, 3), pixel, sample, bounce,
+                      purpose);
 }
 constexpr size_t kUniformsBytes = (sizeof(Uniforms) + 255) / 256 * 256;
 
@@ -186,9 +187,9 @@ __device__ __forceinline__ D3 unit_vector_from(double z, double r, uint32_t w1) 
     return d3(r * c, r * s, z);
 }
 
-// The sample's camera block (purpose 1): (pixel, sample, 0, 1<<24).
+// The sample's camera block (purpose 1): (pixel, sample, 0, 1).
 __device__ __forceinline__ Block camera_block(UniPtr uni, uint32_t pixel, uint32_t sample) {
-    return philox4x32_10(uni_seed(uni), pixel, sample, 0u, kPurposeCamera << 24);
+    return draw(uni, pixel, sample, 0u, kPurposeCamera);
 }
 
 // Camera.GetRay (ray/camera.go:113-142). The sample's camera block `u` feeds the
@@ -774,7 +775,11 @@ __device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, i
     if (p.passes > 1) q = udiv(q, p.div_passes, k);
     const uint32_t tile = q >> 6, r = q & 63u;
     uint32_t tx;
+#ifdef TRAY_TILES_BOTTOM_UP  // A/B only: the band's tile rows issued bottom-up
+    const uint32_t ty = (uint32_t)((p.band_rows + 7) >> 3) - 1u - udiv(tile, p.div_tiles_x, tx);
+#else
     const uint32_t ty = udiv(tile, p.div_tiles_x, tx);
+#endif
     x = (int32_t)(tx * 8u + (r & 7u));
     const int32_t jb = (int32_t)(ty * 8u + (r >> 3));
     j = p.j0 + jb;
@@ -938,7 +943,7 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
 // ended (stored; the lane is free).
 //
 // Written for a wave of lanes on different branches: the work several branches
-// need is done once, before them — the bounce's Philox block and the unit
+// need is done once, before them — the bounce's draw block and the unit
 // direction (sky, Metal, Dielectric).
 template <bool kStats, int kAcc, typename GeoAt, typename MatAt>
 __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
@@ -953,7 +958,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     // instead of starting after it inside the hit branch.
     const double4 g = geo_at();
     const MatRec m = mat_at();
-    const Block w = philox4x32_10(uni_seed(uni), L.pixel, L.sample, L.bounce, kPurposeScatter << 24);
+    const Block w = draw(uni, L.pixel, L.sample, L.bounce, kPurposeScatter);
     const double u0 = uniform(w.x0);
     // Unit(r.Direction) is read by the sky, Metal and Dielectric, not by Lambertian
     // (nor a last-level hit): a wave whose shading lanes are all Lambertian hits
@@ -1154,13 +1159,24 @@ __device__ __forceinline__ void prof_material(int site, bool active, int32_t slo
 #endif
 
 // Diagnostic build only (-DTRAY_PROFILE_TIMELINE, stats instance; tools/timeline.py):
-// per wave, busy lanes integrated over time in kTlTicks buckets of the 100 MHz
+// per wave, busy lanes integrated over time in kTlTicks buckets of the shader clock
+// (s_memtime, read once per loop iteration; the 100 MHz constant clock, s_memrealtime,
+// only at the wave's start, dry point and end: read per iteration it stalled waves),
 // constant clock, relative to the wave's start, plus its start, end, the time its
 // queue ran dry and the chunks it took. Record of wave w at stats[32 + w x kTlStride]:
 // [0] start, [1] end, [2] exhausted (ticks after start), [3] chunks, [4..] buckets.
 #ifdef TRAY_PROFILE_TIMELINE
-constexpr uint32_t kTlBuckets = 1024, kTlTicks = 1000, kTlStride = kTlBuckets + 4;  // 10-us buckets
+// [0] start, [1] end, [2] dry (constant clock), [3] chunks, [4] / [5] shader clock at start / end,
+// [6 ..] buckets, the last three: the wave's last lone path (segments, pixel, sample).
+constexpr uint32_t kTlBuckets = 1024, kTlTicks = 25000, kTlHdr = 6, kTlStride = kTlBuckets + kTlHdr;
 #endif
+
+// Sum of a per-lane 64-bit counter over the wave (instrumented instances only).
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
 
 // Persistent megakernel: waves pull 64-pixel work items from a global counter
 // and lanes refill individually, so no lane idles while the frame has work.
@@ -1206,7 +1222,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         u->bg_b.x = p.bg_b.x, u->bg_b.y = p.bg_b.y, u->bg_b.z = p.bg_b.z;
         u->focus_time = p.focus_time;
         u->ray_radius = p.ray_radius;
-        u->seed = p.seed;
+        for (int k = 0; k < 4; ++k) u->key[k] = p.key[k];
         u->pool = 0;  // empty: the first taker refills it
         u->pool_chunks = p.pool_chunks;
     }
@@ -1299,25 +1315,38 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     unsigned long long* prof_mat = p.stats + 32 + 2 * gridDim.x * (blockDim.x / 64u);
 #endif
 #ifdef TRAY_PROFILE_TIMELINE
-    unsigned long long* tl =
-        p.stats + 32 + (size_t)(blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * kTlStride;
-    const uint64_t tl_start = __builtin_amdgcn_s_memrealtime();
-    uint64_t tl_prev = tl_start, tl_acc = 0;
+    unsigned long long* tl =  // only the stats instance has a buffer; every use is under kStats
+        kStats ? p.stats + 32 + (size_t)(blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * kTlStride : nullptr;
+    const uint64_t tl_start = __builtin_amdgcn_s_memrealtime(), tl_mt0 = __builtin_amdgcn_s_memtime();
+    uint64_t tl_prev = tl_mt0, tl_acc = 0;
     uint32_t tl_busy = 0, tl_bucket = 0, tl_chunks = 0, tl_dry = 0;
 #endif
 
     while (true) {
 #ifdef TRAY_PROFILE_TIMELINE
-        {
-            const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            const uint32_t b = min((uint32_t)((tl_prev - tl_start) / kTlTicks), kTlBuckets - 1u);
+        if constexpr (kStats) {  // p.stats is null in every other instance
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            const uint32_t b = min((uint32_t)((tl_prev - tl_mt0) / kTlTicks), kTlBuckets - 4u);
             if (b != tl_bucket) {
-                if (lane == 0) tl[4 + tl_bucket] = tl_acc;
+                if (lane == 0) tl[kTlHdr + tl_bucket] = tl_acc;
                 tl_bucket = b;
                 tl_acc = 0;
             }
             tl_acc += (now - tl_prev) * tl_busy;
             tl_prev = now;
+            // The wave's last path after its queue ran dry: its segments so far, pixel, sample.
+            const uint64_t m = __ballot(L.busy);
+            if (exhausted && __popcll(m) == 1) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                const uint32_t seg = __builtin_amdgcn_readlane(L.segments, l);
+                const uint32_t pix = __builtin_amdgcn_readlane(L.pixel, l);
+                const uint32_t smp = __builtin_amdgcn_readlane(L.sample, l);
+                if (lane == 0) {
+                    tl[kTlHdr + kTlBuckets - 3] = seg;
+                    tl[kTlHdr + kTlBuckets - 2] = pix;
+                    tl[kTlHdr + kTlBuckets - 1] = smp;
+                }
+            }
         }
 #endif
 #ifndef TRAY_PROFILE_REFILL  // slots 10, 13-15 hold the refill split instead
@@ -1365,7 +1394,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     if (c == kPoolDone) {
                         exhausted = true;
 #ifdef TRAY_PROFILE_TIMELINE
-                        tl_dry = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tl_start);
+                        if constexpr (kStats) tl_dry = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tl_start);
 #endif
                         break;
                     }
@@ -1505,7 +1534,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)prof_cam, lw);
                 const uint64_t h = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(prof_hit >> 32), lw) << 32) |
                                    (uint32_t)__builtin_amdgcn_readlane((uint32_t)prof_hit, lw);
-                PROF_CNT(13, c - prof_assigned);  // decoding + camera ray (Philox, discs)
+                PROF_CNT(13, c - prof_assigned);  // decoding + camera ray (draw block, discs)
                 PROF_CNT(14, h - c);              // out-of-tree spheres + candidates (or the FP32 setup)
             }
         }
@@ -1666,9 +1695,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     if constexpr (kProg) flush_progress(p, prog_cur, prog_cnt, lane);
     if constexpr (kAcc) (void)acc_retire<kAcc>(p, acc, acc_all & ~acc_free, false, 0u, acc_chunk, lane);  // every lane is idle
     if constexpr (kStats) {
-        atomicAdd(p.stats + 0, (unsigned long long)st.segments);
-        atomicAdd(p.stats + 1, (unsigned long long)st.spheres);
-        atomicAdd(p.stats + 2, (unsigned long long)st.boxes);
+        // One atomic per wave: 3 per lane on three addresses serialised ~9 ms of tail
+        // onto every instrumented launch (786 K device-scope atomics at C2).
+        const uint64_t seg_w = wave_sum_u64(st.segments), sph_w = wave_sum_u64(st.spheres),
+                       box_w = wave_sum_u64(st.boxes);
+        if (lane == 0) {
+            atomicAdd(p.stats + 0, (unsigned long long)seg_w);
+            atomicAdd(p.stats + 1, (unsigned long long)sph_w);
+            atomicAdd(p.stats + 2, (unsigned long long)box_w);
+        }
 #if defined(TRAY_STATS_PRIMARY) && !defined(TRAY_PROFILE)
         atomicAdd(p.stats + 3, (unsigned long long)st.nodes0);
         atomicAdd(p.stats + 4, (unsigned long long)st.leaves0);
@@ -1689,12 +1724,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #ifdef TRAY_PROFILE_TIMELINE
     if (kStats && lane == 0) {
         const uint64_t end = __builtin_amdgcn_s_memrealtime();
-        tl_acc += (end - tl_prev) * tl_busy;
-        tl[4 + tl_bucket] = tl_acc;
+        const uint64_t mt_end = __builtin_amdgcn_s_memtime();
+        tl_acc += (mt_end - tl_prev) * tl_busy;
+        tl[kTlHdr + tl_bucket] = tl_acc;
         tl[0] = tl_start;
         tl[1] = end;
         tl[2] = tl_dry;
         tl[3] = tl_chunks;
+        tl[4] = tl_mt0;
+        tl[5] = mt_end;
     }
 #endif
 #ifdef TRAY_PROFILE

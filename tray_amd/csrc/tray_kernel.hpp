@@ -125,7 +125,7 @@ struct KernelParams {
     int32_t out_format;
     double ray_radius;
     double focus_time;  // FocusDistance / FocalLength (ray/camera.go:134)
-    uint64_t seed;
+    uint32_t key[4];  // the draw key of the seed (rng.hpp draw_key, include/tray.h)
     CamRec cam;
     V3 bg_a, bg_b;
     void* out;
