@@ -35,6 +35,9 @@
  *                         for the kernel instance (several per CU for small
  *                         instances; clamped to 0..resident-1), for kernels
  *                         that run beside it: collectives, copies (same bits)
+ *   "work_order"          0: hand a launch's 8x8 tiles out in band order instead of
+ *                         most expensive first by a counting launch's Scene.Hit
+ *                         calls (same bits)
  */
 #ifndef TRAY_DEBUG_H
 #define TRAY_DEBUG_H

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--passes", type=int, default=1,
                     help="frames per launch (tray_render_passes_async); times are per frame")
     ap.add_argument("--lib", default=None, help="a libtray_amd.so build to load (default: the in-tree one)")
+    ap.add_argument("--knob", action="append", default=[], help="NAME=VALUE include/tray_debug.h knob (repeatable)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -39,6 +40,8 @@ def main():
     cam = ray.RichSceneCamera()
     cam.Initialize(W, H)
     lib = os.path.abspath(args.lib) if args.lib else None
+    if args.knob:
+        _lib.set_debug_knobs(lib, **{k: int(v) for k, v in (kv.split("=", 1) for kv in args.knob)})
     scene = _lib.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0, *([lib] if lib else []))
     stream = torch.cuda.current_stream()
     base = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)

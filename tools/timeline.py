@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--waves", type=int, default=256 * 16)
     ap.add_argument("--reps", type=int, default=3, help="renders; the last one is reported")
     ap.add_argument("--curve", action="store_true", help="print the per-bucket utilisation curve too")
+    ap.add_argument("--knob", action="append", default=[], help="NAME=VALUE include/tray_debug.h knob (repeatable)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -40,6 +41,8 @@ def main():
     spheres = ray.rich_scene_array(seed, half)
     cam = ray.RichSceneCamera()
     cam.Initialize(W, H)
+    if args.knob:
+        _lib.set_debug_knobs(os.path.abspath(args.lib), **{k: int(v) for k, v in (kv.split("=", 1) for kv in args.knob)})
     scene = _lib.DeviceScene(spheres, ray._background(ray.DefaultBackground()), 0, os.path.abspath(args.lib))
     params = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGB_F32)
     if args.shard:
@@ -79,7 +82,7 @@ def main():
     t_first = int(first_dry // TICKS)
     q = [0, 1, 10, 50, 90, 99, 100]
     d = {
-        "config": args.config, "shard": args.shard, "shader_ghz": round(float(np.median(100e6 / ratio)) / 1e9, 3), "waves": int(len(rec)), "span_us": round(span / 100, 1),
+        "config": args.config, "shard": args.shard, "knobs": args.knob, "shader_ghz": round(float(np.median(100e6 / ratio)) / 1e9, 3), "waves": int(len(rec)), "span_us": round(span / 100, 1),
         "lane_util_overall": round(busy_total / (span * lanes), 4),
         "first_dry_us": round(first_dry / 100, 1), "last_dry_us": round(last_dry / 100, 1),
         "end_us_pct": {str(k): round(float(np.percentile(end_rel, k)) / 100, 1) for k in q},

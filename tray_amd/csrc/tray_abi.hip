@@ -40,7 +40,7 @@ static std::atomic<long long> g_knob_value[kKnobCount];
 static std::atomic<bool> g_knob_set[kKnobCount];
 static const char* const kKnobNames[kKnobCount] = {
     "acc_slots", "band_samples", "bvh_leaf", "bvh_lds_mode", "stack_lds_slots", "node_deep", "primary_candidates",
-    "resolve_staged", "wave_chunks", "scene_contexts", "grid_reserve"};
+    "resolve_staged", "wave_chunks", "scene_contexts", "grid_reserve", "work_order"};
 
 bool debug_knob(DebugKnob k, long long* v) {
     if (!g_knob_set[k].load(std::memory_order_acquire)) return false;
@@ -196,6 +196,16 @@ struct LaunchCtx {
     CandKey cand_key;
     uint32_t* stack_ovf = nullptr;
     size_t ovf_bytes = 0;
+    // Work order (launch_render): per 8x8 tile of the rows, the Scene.Hit calls a
+    // counting launch measured and the order the next launches hand tiles out in,
+    // valid for `order_key` (camera, rows, tiling, rays per pixel, depth).
+    uint32_t* tile_cost = nullptr;
+    size_t tile_cost_bytes = 0;
+    uint32_t* tile_order = nullptr;
+    size_t tile_order_bytes = 0;
+    bool order_valid = false;
+    CandKey order_key;
+    int32_t order_spp = 0, order_depth = 0;
     hipEvent_t done = nullptr;
     bool launched = false;          // `done` has been recorded
     hipStream_t last_stream = nullptr;
@@ -495,7 +505,7 @@ static void free_ctx(LaunchCtx* c) {
     if (c->launched) (void)hipEventSynchronize(c->done);  // its last render, on whatever stream
     if (c->queue) (void)hipFree(c->queue);
     // Pool allocations (grow_ctx_buffer), idle now: released on the null stream.
-    for (void* b : {(void*)c->samples, (void*)c->cand, (void*)c->stack_ovf})
+    for (void* b : {(void*)c->samples, (void*)c->cand, (void*)c->stack_ovf, (void*)c->tile_cost, (void*)c->tile_order})
         if (b) (void)hipFreeAsync(b, nullptr);
     if (c->done) (void)hipEventDestroy(c->done);
     delete c;
@@ -521,6 +531,11 @@ constexpr int32_t kCandMaxSpheres = 16384;
 static bool cand_enabled() {
     long long v = 1;
     return !debug_knob(kKnobPrimaryCandidates, &v) || v != 0;
+}
+// Expensive-first work order (on unless the "work_order" knob is 0, an A/B and test switch).
+static bool work_order_enabled() {
+    long long v = 1;
+    return !debug_knob(kKnobWorkOrder, &v) || v != 0;
 }
 
 // The fixed-point scale 2^k of a render (tray_kernel.hpp), or 0 for the FP64
@@ -740,14 +755,36 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     k.queue = c->queue;
     k.samples = c->samples;
     k.stack_ovf = c->stack_ovf;
+    CandKey key;  // what the candidate records (and, with r and depth, the work order) depend on
+    memset(&key, 0, sizeof(key));
+    key.cam = *cam;
+    key.ray_radius = p->ray_radius;
+    key.width = p->width, key.height = p->height, key.y_start = p->y_start, key.rows = k.rows;
+    key.tile_rows = k.tile_rows, key.tile_count = k.tile_count, key.tile_index = k.tile_index;
+    key.multi_sample = p->rays_per_pixel > 1;
+    // Work order: the order a counting launch of this key measured, else (with on-chip
+    // sums) count now; the frame's bits do not depend on the order.
+    uint32_t* order_out = nullptr;
+    bool counting = false;
+    if (work_order_enabled()) {
+        const size_t tile_bytes = (size_t)((p->width + 7) / 8) * (size_t)((k.rows + 7) / 8) * sizeof(uint32_t);
+        const bool same = c->order_valid && c->order_spp == p->rays_per_pixel && c->order_depth == p->max_depth &&
+                          memcmp(&key, &c->order_key, sizeof(key)) == 0 && c->tile_order_bytes >= tile_bytes;
+        if (same) {
+            k.tile_order = c->tile_order;
+        } else if (plan.layout.acc_slots > 0) {
+            c->order_valid = false;
+            e = grow_ctx_buffer(reinterpret_cast<void**>(&c->tile_cost), &c->tile_cost_bytes, tile_bytes, stream);
+            if (e == hipSuccess)
+                e = grow_ctx_buffer(reinterpret_cast<void**>(&c->tile_order), &c->tile_order_bytes, tile_bytes, stream);
+            if (e == hipSuccess) e = hipMemsetAsync(c->tile_cost, 0, tile_bytes, stream);
+            if (e != hipSuccess) return finish(e, "work order buffers");
+            k.tile_cost = c->tile_cost;
+            order_out = c->tile_order;
+            counting = true;
+        }
+    }
     if (use_bvh && cand_enabled() && sc->n_slots - sc->n_global <= kCandMaxSpheres) {
-        CandKey key;
-        memset(&key, 0, sizeof(key));
-        key.cam = *cam;
-        key.ray_radius = p->ray_radius;
-        key.width = p->width, key.height = p->height, key.y_start = p->y_start, key.rows = k.rows;
-        key.tile_rows = k.tile_rows, key.tile_count = k.tile_count, key.tile_index = k.tile_index;
-        key.multi_sample = p->rays_per_pixel > 1;
         if (!c->cand_valid || memcmp(&key, &c->cand_key, sizeof(key)) != 0) {
             c->cand_valid = false;
             e = grow_ctx_buffer(reinterpret_cast<void**>(&c->cand), &c->cand_bytes,
@@ -759,7 +796,14 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
         }
         k.cand = c->cand;
     }
-    return finish(launch_render(k, use_bvh, plan, stream, c->samples_bytes), "launch_render");
+    e = launch_render(k, use_bvh, plan, stream, c->samples_bytes, order_out);
+    if (e == hipSuccess && counting) {  // the next launch of this key hands its tiles out by cost
+        c->order_valid = true;
+        c->order_key = key;
+        c->order_spp = p->rays_per_pixel;
+        c->order_depth = p->max_depth;
+    }
+    return finish(e, "launch_render");
 }
 
 int tray_render_plan_get(tray_scene_t sc, const tray_camera* cam, const tray_params* p, int32_t n_passes,

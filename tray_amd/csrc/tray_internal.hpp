@@ -35,6 +35,7 @@ enum DebugKnob {
     kKnobWaveChunks,
     kKnobSceneContexts,
     kKnobGridReserve,
+    kKnobWorkOrder,
     kKnobCount
 };
 // True, with the value in *v, when the knob is set.

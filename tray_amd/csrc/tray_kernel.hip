@@ -278,8 +278,10 @@ struct Lane {
 // KernelParams::acc_rshift (6: one group per chunk; log2 r: 64 / r groups).
 typedef __attribute__((address_space(3))) double LdsF64;
 
+typedef __attribute__((address_space(3))) uint32_t LdsU32;
 struct AccCtx {
-    LdsF64* slabs;  // this wave's slots: groups x kAccCopies x 3 sums each
+    LdsF64* slabs;   // this wave's slots: groups x kAccCopies x 3 sums each
+    LdsU32* counts;  // this wave's slots: Scene.Hit calls of the slot's chunk (work-order cost)
 };
 // kAcc: 1 one group per chunk (64 | r), 2 64 / r pixel-pass groups per chunk (r = 16, 32).
 template <int kAcc>
@@ -768,22 +770,29 @@ __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni
 // (the same surfaces, similar lengths). Ordering the items pass by pass instead
 // cost C2 1.2 %, C5 2.2 %, C1 6.5 % and an 8-way shard 4.6 % (each
 // chunk then went to another pixel).
-__device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, int32_t& x, int32_t& j, uint32_t& s,
-                                            uint32_t& k) {
+// Work order (p.tile_order): the t-th tile of items (q >> 6 == t) renders band tile
+// tile_order[t], looked up once per chunk by the caller (`tile`, chunk_tile);
+// without an order, tile t. A chunk never straddles two tiles (a tile is 64
+// pixels x r x passes items, a multiple of 64).
+__device__ __forceinline__ bool decode_item(const KernelParams& p, uint32_t i, uint32_t tile, int32_t& x, int32_t& j,
+                                            uint32_t& s, uint32_t& k) {
     k = 0;
     uint32_t q = udiv(i, p.div_spp, s);
     if (p.passes > 1) q = udiv(q, p.div_passes, k);
-    const uint32_t tile = q >> 6, r = q & 63u;
+    const uint32_t r = q & 63u;
+    if (!p.tile_order) tile = q >> 6;
     uint32_t tx;
-#ifdef TRAY_TILES_BOTTOM_UP  // A/B only: the band's tile rows issued bottom-up
-    const uint32_t ty = (uint32_t)((p.band_rows + 7) >> 3) - 1u - udiv(tile, p.div_tiles_x, tx);
-#else
     const uint32_t ty = udiv(tile, p.div_tiles_x, tx);
-#endif
     x = (int32_t)(tx * 8u + (r & 7u));
     const int32_t jb = (int32_t)(ty * 8u + (r >> 3));
     j = p.j0 + jb;
     return x < p.width && jb < p.band_rows;
+}
+// The band tile chunk c renders (wave-uniform: one scalar load per chunk taken).
+__device__ __forceinline__ uint32_t chunk_tile(const KernelParams& p, uint32_t c) {
+    if (!p.tile_order) return 0u;  // unused: decode_item takes q >> 6
+    uint32_t rem;
+    return __builtin_amdgcn_readfirstlane(p.tile_order[udiv(c, p.div_chunks_per_tile, rem)]);
 }
 
 // Start sample s of pixel (x, compact row j) in the lane: its camera ray.
@@ -822,6 +831,8 @@ __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D
         __hip_atomic_fetch_add(s + 0, __builtin_rint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(s + 1, __builtin_rint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(s + 2, __builtin_rint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        if (p.tile_cost)  // a counting launch (the work order's costs): the chunk's Scene.Hit calls
+            __hip_atomic_fetch_add(acc.counts + L.slot, L.segments, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     } else {
         double* o = p.samples + (size_t)L.item * 3;
         o[0] = color.x;
@@ -916,6 +927,13 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
     // Each of the slot's groups (one per chunk, or 64 / r pixel-passes) is one record.
     if ((freed >> lane) & 1ull) {
         const uint32_t groups = 64u >> acc_rshift<kAcc>(p);
+        // the chunk's Scene.Hit calls (a counting launch; 0 otherwise) ride in group 0's pad
+        uint32_t count = 0u;
+        if (p.tile_cost) {
+            volatile LdsU32* n = acc.counts;  // after every add of the wave's lanes (LDS issue order)
+            count = n[lane];
+            n[lane] = 0u;
+        }
         for (uint32_t g = 0; g < groups; ++g) {
             const uint32_t slab = kAcc == 1 ? lane : lane * groups + g;
             volatile LdsF64* v = acc.slabs + slab * kAccCopies * 3u;
@@ -930,6 +948,7 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
             o->sum[0] = sum[0];
             o->sum[1] = sum[1];
             o->sum[2] = sum[2];
+            o->pad = g == 0 ? (double)count : 0.0;
             if constexpr (kAcc == 1) break;
         }
     }
@@ -1273,8 +1292,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         for (int i = threadIdx.x; i < p.n_pad; i += blockDim.x) smem[i] = p.geo[i];
         sv.geo = smem;
     }
-    // [acc: waves x acc_slots x groups x kAccSlotBytes] at acc_off
-    AccCtx acc{nullptr};
+    // [acc: waves x acc_slots x groups x kAccSlotBytes][counts: waves x acc_slots x 4 B] at acc_off
+    AccCtx acc{nullptr, nullptr};
     uint64_t acc_free = 0;   // kAcc, wave-uniform: free slots
     uint64_t acc_all = 0;    // kAcc, wave-uniform: every slot
     uint32_t acc_chunk = 0;  // kAcc: lane s holds the chunk of slot s
@@ -1284,6 +1303,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         const uint32_t slots = (uint32_t)p.acc_slots;
         for (uint32_t i = threadIdx.x; i < waves * slots * slot_f64; i += blockDim.x) all[i] = 0.0;
         acc.slabs = all + (threadIdx.x / 64u) * slots * slot_f64;
+        LdsU32* counts = (LdsU32*)(all + waves * slots * slot_f64);
+        for (uint32_t i = threadIdx.x; i < waves * slots; i += blockDim.x) counts[i] = 0u;
+        acc.counts = counts + (threadIdx.x / 64u) * slots;
         acc_free = acc_all = slots >= 64u ? ~0ull : (1ull << slots) - 1ull;
     }
     __syncthreads();
@@ -1298,6 +1320,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     uint32_t grp_next = 0, grp_end = 0;    // wave-uniform: the rest of the wave's reserved chunks
 
     uint32_t pool_slot = 0;                 // kAcc, wave-uniform: the current chunk's accumulator slot
+    uint32_t pool_tile = 0;                 // wave-uniform: the band tile the current chunk renders (work order)
     bool exhausted = false;
 #ifdef TRAY_STATS_GROUND
     uint32_t gcls = 0;  // diagnostic: class of the lane's current segment (1/2: from an out-of-tree sphere, up / other)
@@ -1359,7 +1382,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         if (__popcll(idle) < TRAY_REFILL_BATCH && idle != ~0ull) idle = 0ull;  // batch refills
         // Items are assigned first (cheap, may span two chunks); the camera rays of
         // all newly assigned lanes are then generated together.
-        uint32_t fresh_item = ~0u, fresh_slot = 0u;
+        uint32_t fresh_item = ~0u, fresh_slot = 0u, fresh_tile = 0u;
         bool cam_hit = false;  // a camera ray whose Scene.Hit the candidate list answered in this refill
 #ifdef TRAY_PROFILE_CANDWAIT
         uint64_t prof_wait = 0;
@@ -1406,13 +1429,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 }
                 pool_next = c * 64u;
                 pool_end = pool_next + 64u;
+                pool_tile = chunk_tile(p, c);
                 if constexpr (kAcc) {
                     // With 64 | r every item of a chunk is one pixel's: valid or padding
                     // together. A chunk of several pixel-passes (r | 64) may mix the two
                     // and always takes a slot (its padding groups retire as zeros).
                     int32_t cx, cj;
                     uint32_t cs, cp;
-                    if (acc_rshift<kAcc>(p) < 6u || (pool_next < p.items && decode_item(p, pool_next, cx, cj, cs, cp))) {
+                    if (acc_rshift<kAcc>(p) < 6u ||
+                        (pool_next < p.items && decode_item(p, pool_next, pool_tile, cx, cj, cs, cp))) {
                         pool_slot = (uint32_t)__builtin_ctzll(acc_free);
                         acc_free &= ~(1ull << pool_slot);
                         acc_chunk = lane == pool_slot ? c : acc_chunk;
@@ -1426,6 +1451,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 if (rank < take) {
                     fresh_item = pool_next + rank;
                     fresh_slot = pool_slot;
+                    fresh_tile = pool_tile;
                 }
             }
             pool_next += take;
@@ -1445,7 +1471,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             TRAY_MARK("refill_cam")
             int32_t x, j;
             uint32_t smp, pass;
-            if (fresh_item < p.items && decode_item(p, fresh_item, x, j, smp, pass)) {
+            if (fresh_item < p.items && decode_item(p, fresh_item, fresh_tile, x, j, smp, pass)) {
 #ifdef TRAY_PROBE_REFILL
                 TRAY_PROBE_F32(TRAY_PROBE_REFILL)
 #endif
@@ -1806,12 +1832,22 @@ __global__ __launch_bounds__(256) void resolve_kernel(KernelParams p) {
     const uint32_t pix_stride = p.passes * (uint32_t)p.spp;  // items between consecutive pixels of a pass
     int32_t x, j;
     uint32_t s0, pass;
-    const bool valid = decode_item(p, item0, x, j, s0, pass);
+    // A wave's 64 pixels are one tile of the item order (q >> 6): one work-order lookup.
+    const uint32_t tile = p.tile_order ? __builtin_amdgcn_readfirstlane(p.tile_order[q >> 6]) : 0u;
+    const bool valid = decode_item(p, item0, tile, x, j, s0, pass);
     D3 sum = d3(0, 0, 0);
     if constexpr (kMode == kResolvePartials) {
-        if (!valid) return;
         // One record per 64 items (64 | r: r / 64 per pixel-pass) or per pixel-pass (r | 64).
         const AccPartial* part = reinterpret_cast<const AccPartial*>(p.samples) + (item0 >> p.acc_rshift);
+        if (p.tile_cost) {  // a counting launch: the tile's Scene.Hit calls for the next work order
+            uint64_t n = 0;
+            if (valid)
+                for (int32_t c = 0; c < (p.spp >> p.acc_rshift); ++c) n += (uint64_t)part[c].pad;
+            n = wave_sum_u64(n);
+            if ((threadIdx.x & 63u) == 0u)
+                atomicAdd(p.tile_cost + (p.tile_order ? tile : q >> 6), (uint32_t)min<uint64_t>(n, 0xFFFFFFFFull));
+        }
+        if (!valid) return;
         int64_t s[3] = {0, 0, 0};
         uint32_t bad = 0u;
         for (int32_t c = 0; c < (p.spp >> p.acc_rshift); ++c)
@@ -2074,6 +2110,38 @@ static KernelFn pick_kernel2(int lds_mode, bool stats, bool progress, bool deep)
     return pick_kernel3<kBVH, kSpill, false, false, kAcc>(lds_mode, deep);
 }
 
+// The next launch's work order from a counting launch's tile costs (one
+// workgroup; launch_render runs it after a band's resolve): the band's tiles by
+// decreasing Scene.Hit calls, a counting sort over 256 logarithmic buckets (12
+// per octave), so a launch hands out its most expensive tiles first and ends on
+// cheap ones. A tile's longest paths (50 segments at C2) then start early instead
+// of holding the last waves of the grid alone ("Work order"). The
+// order inside a bucket is whatever the LDS atomics give: it changes the
+// schedule, never a pixel (every pixel's sum is order-free). Zeroes the costs.
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t c) {
+    return c == 0u ? 0u : min(255u, 1u + (uint32_t)(__builtin_log2f((float)c) * 12.0f));
+}
+__global__ __launch_bounds__(1024) void tile_order_kernel(uint32_t* cost, uint32_t* order, uint32_t n) {
+    __shared__ uint32_t slot[256];
+    for (uint32_t b = threadIdx.x; b < 256u; b += blockDim.x) slot[b] = 0u;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) atomicAdd(&slot[cost_bucket(cost[t])], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive prefix over the buckets, most expensive first
+        uint32_t run = 0u;
+        for (int b = 255; b >= 0; --b) {
+            const uint32_t c = slot[b];
+            slot[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+        order[atomicAdd(&slot[cost_bucket(cost[t])], 1u)] = t;
+        cost[t] = 0u;
+    }
+}
+
 // On-chip accumulation is built for the BVH kernel with the whole stack on
 // chip (launch_layout grants accumulators only then); every other launch sums
 // through the per-sample buffer.
@@ -2220,7 +2288,8 @@ LaunchLayout launch_layout(const KernelParams& p, bool use_bvh) {
             (acc_record_shift(p.spp) == 6u || L.lds_mode == 1)) {  // groups: one kernel instance (scene in LDS)
             const uint32_t rshift = acc_record_shift(p.spp);
             const size_t waves = (size_t)kBvhBlock / 64u;
-            const size_t per_slot = waves * kAccSlotBytes * (64u >> rshift);  // every group of a chunk
+            // every group of a chunk, and the chunk's Scene.Hit count (work order)
+            const size_t per_slot = waves * (kAccSlotBytes * (64u >> rshift) + kAccCountBytes);
             const size_t left = kMaxLDSBytes - L.lds;
             int32_t slots = (int32_t)std::min<size_t>(kAccSlotsMax, left / per_slot);
             const bool forced = debug_knob(kKnobAccSlots, &knob);  // tests / A-B: fewer slots, 0 = off
@@ -2255,7 +2324,7 @@ LaunchPlan plan_launch(const KernelParams& p, bool use_bvh) {
 }
 
 hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, hipStream_t stream,
-                         size_t samples_bytes) {
+                         size_t samples_bytes, uint32_t* order_out) {
     if (p.rows <= 0) return hipSuccess;
     if (p.passes < 1) p.passes = 1;
     const uint64_t spp_launch = (uint64_t)p.spp * p.passes;
@@ -2265,6 +2334,10 @@ hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, h
     p.div_spp = make_fastdiv((uint32_t)p.spp);
     p.div_tiles_x = make_fastdiv((uint32_t)p.tiles_x);
     p.div_tile_rows = make_fastdiv((uint32_t)std::max(p.tile_rows, 1));
+    p.div_chunks_per_tile = make_fastdiv((uint32_t)spp_launch);  // a tile: 64 pixels x r x passes items
+    if (p.tile_cost && (!order_out || p.acc_slots <= 0)) return hipErrorInvalidValue;  // counting needs both
+    const uint32_t* order_base = p.tile_order;
+    uint32_t* cost_base = p.tile_cost;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -2337,6 +2410,10 @@ hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, h
     for (int32_t j0 = 0; j0 < p.rows; j0 += band) {
         p.j0 = j0;
         p.band_rows = std::min(band, p.rows - j0);
+        const size_t tile_off = (size_t)(j0 / 8) * (size_t)p.tiles_x;  // the band's tiles in the launch's numbering
+        const uint32_t band_tiles_n = (uint32_t)p.tiles_x * (uint32_t)((p.band_rows + 7) / 8);
+        p.tile_order = order_base ? order_base + tile_off : nullptr;
+        p.tile_cost = cost_base ? cost_base + tile_off : nullptr;
         const uint32_t pixels = (uint32_t)p.tiles_x * (uint32_t)((p.band_rows + 7) / 8) * 64u;
         p.frame_items = pixels * (uint32_t)p.spp;
         p.div_passes = make_fastdiv(p.passes);
@@ -2364,6 +2441,12 @@ hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, h
         if (e != hipSuccess) {
             (void)hipMemsetAsync(p.queue, 0, sizeof(uint32_t), stream);  // keep the invariant
             return e;
+        }
+        if (p.tile_cost) {  // a counting launch: this band's next work order (after its megakernel read the old one)
+            hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, p.tile_cost, order_out + tile_off,
+                               band_tiles_n);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
         }
     }
     return hipSuccess;

@@ -133,6 +133,14 @@ struct KernelParams {
     const double* srgb;  // TRAY_OUT_RGBA8: the 256-entry encoder table (tray::srgb_thresholds)
     unsigned long long* progress;  // nullable, HOST-mapped: samples finished per 8-row tile row of the compact rows
     const uint4* cand;   // nullable (BVH only): primary-ray candidate record per compact pixel (launch_cand_build)
+    // Expensive-first work order ("Work order"; on-chip sums only), per band:
+    // tile_order (nullable: band order) lists the band's 8x8 tiles in the order their
+    // work items are handed out; tile_cost (nullable: no counting) receives each tile's
+    // Scene.Hit calls (the chunk records carry their counts, the resolve adds them), from
+    // which launch_render's tile_order_kernel builds the next launch's order.
+    const uint32_t* tile_order;
+    uint32_t* tile_cost;
+    FastDiv div_chunks_per_tile;  // 64-item chunks per tile: rays_per_pixel x passes
 };
 
 struct LaunchPlan;
@@ -140,8 +148,11 @@ struct LaunchPlan;
 // megakernel and resolve pass of every band. `samples_bytes` is the capacity
 // of p.samples, sized from plan.buffer_bytes by the caller (an internal
 // invariant, checked: hipErrorInvalidValue before anything is enqueued).
+// With p.tile_cost set (a counting launch; on-chip sums only), `order_out` (one
+// word per tile of p's rows) receives the next launch's work order; p.tile_order
+// may be the same buffer (each band's order is rewritten after its megakernel).
 hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, hipStream_t stream,
-                         size_t samples_bytes);
+                         size_t samples_bytes, uint32_t* order_out = nullptr);
 
 // Fixed-point accumulation. A sample's colour c (already scaled by 2^k through
 // the background) is rounded to the integer v = rint(c), |v| <= 2^kAccBits; any
@@ -166,6 +177,8 @@ static_assert(sizeof(AccPartial) == 32, "AccPartial layout");
 #endif
 constexpr int32_t kAccCopies = TRAY_ACC_COPIES;
 constexpr size_t kAccSlotBytes = (size_t)kAccCopies * 3 * sizeof(double);
+// Per slot also one 32-bit count of the chunk's Scene.Hit calls (the work order's cost).
+constexpr size_t kAccCountBytes = sizeof(uint32_t);
 constexpr int32_t kAccSlotsMax = 64;  // per wave (the free-slot mask is 64 bits)
 constexpr int32_t kAccSlotsMin = 8;
 
