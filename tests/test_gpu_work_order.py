@@ -81,3 +81,38 @@ def test_work_order_follows_the_camera(L, O):
     want = [L.render(sc, bg_struct(L, DEFAULT_BG), st, p, 0)[0] for st in (st1, st2)]
     for g, st in zip(got, (0, 1, 0, 0, 1)):
         assert np.array_equal(g, want[st])
+
+
+def test_work_order_with_band_changes(L, O, knobs):
+    """One context alternating one-band launches (which count and then use an
+    order) with multi-band launches of the same key (which must not use it: a
+    band's tiles are numbered within the band): every frame equals band order."""
+    import torch
+
+    sc = O.rich_scene(2)
+    w, h, spp = 72, 45, 64
+    st = camera(L, RICH_SETUP, w, h)
+    p = L.make_params(w, h, 50, spp, 0.5, 3, output=L.OUT_RGB_F64)
+    knobs(band_samples=9 * 64 * spp * 6)  # one band at 1 pass, three at 3 passes
+    seq = (1, 3, 1, 1, 3, 1)
+
+    def run(dev):
+        out = []
+        for n in seq:
+            out += [f for f in _frames(L, torch, dev, st, p, n, 1)[0]]
+        return out
+
+    dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
+    try:
+        assert dev.plan(st, p, 1).acc_slots > 0
+        ordered = run(dev)
+    finally:
+        dev.release()
+    with L.debug_knobs(work_order=0):
+        dev = L.DeviceScene(sc, bg_struct(L, DEFAULT_BG), 0)
+        try:
+            plain = run(dev)
+        finally:
+            dev.release()
+    for a, b in zip(ordered, plain):
+        assert np.array_equal(a, b)

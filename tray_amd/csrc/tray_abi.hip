@@ -766,7 +766,14 @@ static int render_async_impl(tray_scene_t sc, const tray_camera* cam, const tray
     // sums) count now; the frame's bits do not depend on the order.
     uint32_t* order_out = nullptr;
     bool counting = false;
-    if (work_order_enabled()) {
+    // One launch band only: an order lists the band's tiles, so it holds for any launch of
+    // the key with the same (single) band; multi-band launches (C3-C5 at 16 frames) keep
+    // band order and neither use nor count one.
+    // Live progress (tray_render_progress) keeps band order too: rows then finish from the
+    // top as in Go's RenderLines (ray/tracer.go:126-128), where cost order would finish every
+    // row near the end.
+    const bool one_band = (int64_t)plan.band_tiles * 8 >= (int64_t)k.rows;
+    if (work_order_enabled() && one_band && !progress_device) {
         const size_t tile_bytes = (size_t)((p->width + 7) / 8) * (size_t)((k.rows + 7) / 8) * sizeof(uint32_t);
         const bool same = c->order_valid && c->order_spp == p->rays_per_pixel && c->order_depth == p->max_depth &&
                           memcmp(&key, &c->order_key, sizeof(key)) == 0 && c->tile_order_bytes >= tile_bytes;

@@ -740,14 +740,6 @@ __device__ __forceinline__ uint32_t take_chunk(const KernelParams& p, UniPtr uni
             const uint32_t pool_chunks = __builtin_amdgcn_readfirstlane(uni->pool_chunks);
             if (lane == 0) base = atomicAdd(p.queue, pool_chunks);
             base = __builtin_amdgcn_readlane(base, 0);
-#ifdef TRAY_GUIDED_POOL
-            {  // the next refill's size from what this one left in the queue (guided self-scheduling)
-                const uint32_t after = base + pool_chunks;
-                const uint32_t left = after < p.nchunks ? p.nchunks - after : 0u;
-                const uint32_t want = max(1u, min(p.pool_chunks, left / (gridDim.x * (uint32_t)TRAY_GUIDED_POOL)));
-                if (lane == 0) ((volatile __attribute__((address_space(3))) Uniforms*)uni)->pool_chunks = want;
-            }
-#endif
             const uint64_t fresh = base >= p.nchunks
                                        ? (uint64_t)kPoolDone << 32
                                        : ((uint64_t)min(base + pool_chunks, p.nchunks) << 32) | base;
@@ -831,8 +823,17 @@ __device__ __forceinline__ void end_path(const KernelParams& p, Lane& L, const D
         __hip_atomic_fetch_add(s + 0, __builtin_rint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(s + 1, __builtin_rint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_fetch_add(s + 2, __builtin_rint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        if (p.tile_cost)  // a counting launch (the work order's costs): the chunk's Scene.Hit calls
+        // A counting launch (the work order's costs): the chunk's sum of squared path lengths
+        // (Scene.Hit calls per path, squared): a tile's few long paths - a glass rim among sky
+        // pixels - decide when its last sample ends, and squares rank it by them.
+#ifdef TRAY_WO_LINEAR_COST  // A/B only: the plain sum of Scene.Hit calls
+        if (p.tile_cost)
             __hip_atomic_fetch_add(acc.counts + L.slot, L.segments, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
+        if (p.tile_cost)
+            __hip_atomic_fetch_add(acc.counts + L.slot, L.segments * L.segments, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
     } else {
         double* o = p.samples + (size_t)L.item * 3;
         o[0] = color.x;
@@ -2335,7 +2336,7 @@ hipError_t launch_render(KernelParams p, bool use_bvh, const LaunchPlan& plan, h
     p.div_tiles_x = make_fastdiv((uint32_t)p.tiles_x);
     p.div_tile_rows = make_fastdiv((uint32_t)std::max(p.tile_rows, 1));
     p.div_chunks_per_tile = make_fastdiv((uint32_t)spp_launch);  // a tile: 64 pixels x r x passes items
-    if (p.tile_cost && (!order_out || p.acc_slots <= 0)) return hipErrorInvalidValue;  // counting needs both
+    if (p.tile_cost && (!order_out || plan.layout.acc_slots <= 0)) return hipErrorInvalidValue;  // counting needs both
     const uint32_t* order_base = p.tile_order;
     uint32_t* cost_base = p.tile_cost;
     int dev = 0;
