@@ -3,7 +3,7 @@
 # configs given, so every bench line carries traffic and utilisation again.
 #   usage: tools/profile_configs.sh c2 c1 ...
 set -u
-O=gpurun_out/prof; mkdir -p $O
+O=${O:-gpurun_out/prof}; mkdir -p $O
 for c in "$@"; do
   bash tools/gpu_profile_all.sh $O/$c $c || { echo "profile $c failed"; exit 1; }
   echo "profiled $c"

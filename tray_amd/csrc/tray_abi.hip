@@ -888,14 +888,14 @@ static int cached_scene(Slot& sl, const tray_sphere* spheres, int32_t n, const t
             // contexts are idle: the new scene takes them over (their sample and
             // candidate buffers) instead of allocating its own (a C2 frame's 1.4-GB
             // sample buffer: 0.28 ms of hipFree + hipMalloc per new scene,
-            // profiles/r2g_e2e_breakdown.jsonl). Their candidate lists were the
-            // old scene's.
+            // profiles/r2g_e2e_breakdown.jsonl). Their candidate lists and work
+            // orders were the old scene's.
             {
                 std::lock_guard<std::mutex> la(old->mu);
                 std::lock_guard<std::mutex> lb(sc->mu);
                 std::swap(sc->ctx, old->ctx);
                 std::swap(sc->launches, old->launches);
-                for (LaunchCtx* c : sc->ctx) c->cand_valid = false;
+                for (LaunchCtx* c : sc->ctx) c->cand_valid = c->order_valid = false;
             }
             tray_scene_release(old);
         }
