@@ -1608,11 +1608,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 for (int s = 0; s < kSteps; ++s) {
                     const uint64_t m = __ballot(is_trav(T.cur));
                     if (m == 0ull) break;
-#ifdef TRAY_DRAIN_STEPS  // A/B: a wave whose queue ran dry runs every node step of the loop
-                    if (s >= TRAY_NODE_STEPS && __popcll(m) < TRAY_NODE_MORE_LANES && !exhausted) break;
-#else
                     if (s >= TRAY_NODE_STEPS && __popcll(m) < TRAY_NODE_MORE_LANES) break;
-#endif
                     PROF_CNT(4, 1);
                     PROF_CNT(5, __popcll(m));
                     PROF_CNT(11, __popcll(__ballot(is_leaf(T.cur))));             // waiting for the leaf phase
