@@ -10,7 +10,7 @@ same scene, medians of --reps:
   d2h_pageable_ms   hipMemcpy of the RGBA8 frame (3.7 MB) into pageable host memory
   d2h_pinned_ms     the same into pinned host memory
 
-    python tools/e2e_split.py [--config c2] [--reps 7]
+    python tools/e2e_split.py [--config c2] [--reps 7] [--knob work_order=0]
 """
 import argparse
 import json
@@ -26,12 +26,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--knob", action="append", default=[], help="NAME=VALUE include/tray_debug.h knob (repeatable)")
     args = ap.parse_args()
     import numpy as np
     import torch
 
     from bench import CONFIGS
     from tray_amd import _lib, ray
+
+    if args.knob:
+        _lib.set_debug_knobs(None, **{k: int(v) for k, v in (kv.split("=", 1) for kv in args.knob)})
 
     _, seed, half, W, H, spp, depth = CONFIGS[args.config]
     spheres = ray.rich_scene_array(seed, half)
@@ -50,7 +54,7 @@ def main():
             ts.append((time.perf_counter() - t0) * 1e3)
         return round(float(np.median(ts)), 4)
 
-    rec = {"config": args.config, "e2e_ms": med(lambda: _lib.render(spheres, bg, cam._state, p))}
+    rec = {"config": args.config, "knobs": args.knob, "e2e_ms": med(lambda: _lib.render(spheres, bg, cam._state, p))}
     dev = _lib.DeviceScene(spheres, bg, 0)
     out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()

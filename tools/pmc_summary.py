@@ -25,6 +25,10 @@ KERNELS = {k: f", true, false, false, false, {k}, " for k in (0, 1, 2)}
 KERNEL = KERNELS[1]
 
 
+ACC_WHAT = {1: "on-chip accumulation, one record per 64-sample chunk",
+            2: "on-chip accumulation, one record per pixel-pass", 0: "per-sample buffer"}
+
+
 def acc_mode(spp):
     return 1 if spp % 64 == 0 else 2 if spp in (16, 32) else 0
 
@@ -85,16 +89,17 @@ def main():
         "config": args.config,
         "code_object_sha256": code_hash(d),
         "frames_per_launch": args.frames,
-        "kernel": f"tray::render_kernel<L, true, false, false, false, {str(spp % 64 == 0).lower()}, S> (BVH, LDS layout L, "
-                  f"no stack spill, {'on-chip accumulation' if spp % 64 == 0 else 'per-sample buffer'}, S node steps)",
+        "kernel": f"tray::render_kernel<L, true, false, false, false, {acc_mode(spp)}, S> (BVH, LDS layout L, "
+                  f"no stack spill, {ACC_WHAT[acc_mode(spp)]}, S node steps)",
         "bands_per_launch": bands,
         "FETCH_SIZE_KB_raw_per_dispatch": fetch_kb,
         "WRITE_SIZE_KB_per_dispatch": write_kb,
         "fetch_bytes_corrected": fetch,
         "write_bytes": write,
         "hbm_bytes_per_launch": int(fetch + write),
-        "note": "megakernel only, per launch (frames_per_launch frames). With on-chip accumulation (64 | r) it "
-                "writes one 32-B record of fixed-point sums per 64-sample chunk and reads the primary-ray "
+        "note": "megakernel only, per launch (frames_per_launch frames). With on-chip accumulation it writes one "
+                "32-B record of fixed-point sums per 64-sample chunk (64 | r) or per pixel-pass (r = 16, 32) and "
+                "reads the primary-ray "
                 "candidate records (16 B per pixel per frame); without it, one 24-B colour per sample. The "
                 "resolve kernel reads the records back and writes the frames.",
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md HBM "
