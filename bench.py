@@ -624,7 +624,7 @@ def e2e_timings(_lib, spheres, bg, cam, W, H, depth, spp, seed):
     buffer; tools/hip_setup_costs.hip measures ~8 ms each). `e2e_ms_new_scene`:
     the next call, with the config's scene not yet on the device (BVH build,
     upload, sample-buffer allocation, render, copy). `e2e_ms`: the same scene
-    again (the library keeps the last scene it uploaded), median of 3.
+    again (the library keeps the last scene it uploaded), median of 7.
     `e2e_ms_new_scene_warm`: three more scenes the device has not seen (one
     sphere nudged), median: a new scene once the buffers exist."""
     import numpy as np
@@ -637,7 +637,7 @@ def e2e_timings(_lib, spheres, bg, cam, W, H, depth, spp, seed):
     first = (time.perf_counter() - t0) * 1e3
     p = _lib.make_params(W, H, depth, spp, 0.5, seed, output=_lib.OUT_RGBA8)
     ts = []
-    for _ in range(4):
+    for _ in range(8):
         t0 = time.perf_counter()
         _lib.render(spheres, bg, cam._state, p)
         ts.append((time.perf_counter() - t0) * 1e3)

@@ -6,7 +6,7 @@ launch into its dispatches (megakernel, resolve, tile order) and the gaps
 between them.
 
     rocprofv3 --kernel-trace -d DIR -o kt -- python3 tools/launch_anatomy.py --config c1 --reps 30 > run.json
-    python3 tools/launch_anatomy.py --summarize DIR/.../kt_kernel_trace.csv [--run run.json]
+    python3 tools/launch_anatomy.py --summarize DIR/kt_results.db (or a kt_kernel_trace.csv) [--run run.json]
 
 The run prints one JSON line (event-timed ms per launch, median / mean); the
 summary prints, per dispatch kind, the median duration and the median gap from
@@ -35,11 +35,20 @@ def summarize(path, run_path=None):
     import numpy as np
 
     rows = []
-    with open(path, newline="") as f:
-        for r in csv.DictReader(f):
-            k = kind(r["Kernel_Name"])
-            if k:
-                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
+    if path.endswith(".db"):  # rocprofv3's default rocpd (SQLite) output
+        import sqlite3
+
+        with sqlite3.connect(path) as db:
+            for name, start, end in db.execute("select name, start, end from kernels"):
+                k = kind(name)
+                if k:
+                    rows.append((int(start), int(end), k))
+    else:
+        with open(path, newline="") as f:
+            for r in csv.DictReader(f):
+                k = kind(r["Kernel_Name"])
+                if k:
+                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
     rows.sort()
     launches, cur = [], []
     for s, e, k in rows:  # a launch starts at each megakernel dispatch
@@ -108,7 +117,7 @@ def main():
     ap.add_argument("--config", default="c1")
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--rgba", action="store_true", help="RGBA8 output (the drop-in call's format)")
-    ap.add_argument("--summarize", default=None, help="a rocprofv3 kernel_trace.csv of a run")
+    ap.add_argument("--summarize", default=None, help="a rocprofv3 kernel trace of a run (rocpd .db or kernel_trace.csv)")
     ap.add_argument("--run", default=None, help="the run's JSON output (for the event-timed span)")
     args = ap.parse_args()
     if args.summarize:

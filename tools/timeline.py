@@ -60,7 +60,9 @@ def main():
     seen = rec[:, 1] > 0
     rec = rec[seen]
     last = rec[:, HDR + BUCKETS - 3:HDR + BUCKETS].astype(np.int64)  # last path: segments, pixel, sample
-    rec[:, HDR + BUCKETS - 3:] = 0
+    lone_t, lone_seg = rec[:, HDR + BUCKETS - 5].copy(), rec[:, HDR + BUCKETS - 4].astype(np.int64)
+    lone_ph = rec[:, HDR + BUCKETS - 9:HDR + BUCKETS - 5].copy()  # shader ticks: refill, node, leaf, shade
+    rec[:, HDR + BUCKETS - 9:] = 0
     start, end, dry, chunks = rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3]
     ratio = (end - start) / np.maximum(rec[:, 5] - rec[:, 4], 1)  # constant-clock ticks per shader tick
     g0 = start.min()
@@ -69,7 +71,7 @@ def main():
     nb = int(span // TICKS) + 2
     curve = np.zeros(nb)
     for w in range(len(rec)):
-        b = rec[w, HDR:HDR + BUCKETS - 3] * ratio[w]  # busy lane x constant-clock ticks
+        b = rec[w, HDR:HDR + BUCKETS - 9] * ratio[w]  # busy lane x constant-clock ticks
         mid = start[w] - g0 + (np.arange(b.size) + 0.5) * MT_TICKS * ratio[w]
         idx = np.minimum((mid // TICKS).astype(np.int64), nb - 1)
         np.add.at(curve, idx, b)
@@ -103,6 +105,24 @@ def main():
     d["last_path_segments_pct"] = {str(k): float(np.percentile(seg_all, k)) for k in q} if seg_all.size else None
     drain = (end - start - dry)[has_dry] / 100
     d["wave_drain_us_pct"] = {str(k): round(float(np.percentile(drain, k)), 1) for k in q}
+    # the lone path's latency per segment: from the moment it was the wave's only path
+    # to the wave's end, over the segments it traced in that time
+    lone = (lone_t > 0) & (last[:, 0] > lone_seg)
+    if lone.any():
+        dt = (rec[:, 5] - rec[:, 4] - lone_t)[lone] * ratio[lone] / 100  # us
+        dseg = (last[:, 0] - lone_seg)[lone]
+        lone_start = (start + lone_t * ratio - g0)[lone]
+        alive = np.array([(end_rel > t).sum() for t in lone_start])  # waves alive then (of the grid)
+        per = dt / dseg
+        d["lone_path_us_per_segment_pct"] = {str(k): round(float(np.percentile(per, k)), 2) for k in q}
+        d["lone_segments_pct"] = {str(k): float(np.percentile(dseg, k)) for k in q}
+        d["lone_waves"] = int(lone.sum())
+        late = lone_start >= np.percentile(lone_start, 90)  # the last tenth to go lone
+        d["lone_late_us_per_segment_median"] = round(float(np.median(per[late])), 2)
+        d["lone_late_waves_alive_median"] = int(np.median(alive[late]))
+        ph = (lone_ph[lone] * ratio[lone, None] / 100) / dseg[:, None]  # us per segment per phase
+        d["lone_phase_us_per_segment_median"] = dict(zip(("refill", "node", "leaf", "shade"),
+                                                         (round(float(v), 3) for v in np.median(ph, axis=0))))
     if args.curve:
         d["util_curve"] = [round(float(u), 3) for u in util]
     print(json.dumps(d), flush=True)

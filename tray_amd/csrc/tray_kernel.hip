@@ -1131,6 +1131,13 @@ constexpr int32_t kDeepNodes = 384;
         const unsigned long long v_ = (v);                 \
         if (lane == 0) atomicAdd(prof + (slot), v_);       \
     }
+#elif defined(TRAY_PROFILE_TIMELINE)
+// The timeline build times the phases of a wave's lone last path (refill, node steps,
+// leaves, shading: tl_ph[0..3]).
+#define PROF_T0() const uint64_t prof_t0_ = (kStats && tl_lone) ? __builtin_amdgcn_s_memtime() : 0
+#define PROF_ADD(slot) \
+    if (kStats && tl_lone) tl_ph[slot] += __builtin_amdgcn_s_memtime() - prof_t0_
+#define PROF_CNT(slot, v)
 #else
 #define PROF_T0()
 #define PROF_ADD(slot)
@@ -1187,7 +1194,10 @@ __device__ __forceinline__ void prof_material(int site, bool active, int32_t slo
 // [0] start, [1] end, [2] exhausted (ticks after start), [3] chunks, [4..] buckets.
 #ifdef TRAY_PROFILE_TIMELINE
 // [0] start, [1] end, [2] dry (constant clock), [3] chunks, [4] / [5] shader clock at start / end,
-// [6 ..] buckets, the last three: the wave's last lone path (segments, pixel, sample).
+// [6 ..] buckets; the last nine: the shader ticks the wave's lone last path spent in the
+// refill, node-step, leaf and shading phases, when it became the wave's only path
+// (shader ticks after the start) and its segments then, and that path's segments,
+// pixel and sample at the end (its latency per segment with no other path in the wave).
 constexpr uint32_t kTlBuckets = 1024, kTlTicks = 25000, kTlHdr = 6, kTlStride = kTlBuckets + kTlHdr;
 #endif
 
@@ -1344,13 +1354,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     const uint64_t tl_start = __builtin_amdgcn_s_memrealtime(), tl_mt0 = __builtin_amdgcn_s_memtime();
     uint64_t tl_prev = tl_mt0, tl_acc = 0;
     uint32_t tl_busy = 0, tl_bucket = 0, tl_chunks = 0, tl_dry = 0;
+    bool tl_lone = false;
+    uint64_t tl_ph[4] = {0, 0, 0, 0};
 #endif
 
     while (true) {
 #ifdef TRAY_PROFILE_TIMELINE
         if constexpr (kStats) {  // p.stats is null in every other instance
             const uint64_t now = __builtin_amdgcn_s_memtime();
-            const uint32_t b = min((uint32_t)((tl_prev - tl_mt0) / kTlTicks), kTlBuckets - 4u);
+            const uint32_t b = min((uint32_t)((tl_prev - tl_mt0) / kTlTicks), kTlBuckets - 10u);
             if (b != tl_bucket) {
                 if (lane == 0) tl[kTlHdr + tl_bucket] = tl_acc;
                 tl_bucket = b;
@@ -1366,10 +1378,15 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 const uint32_t pix = __builtin_amdgcn_readlane(L.pixel, l);
                 const uint32_t smp = __builtin_amdgcn_readlane(L.sample, l);
                 if (lane == 0) {
+                    if (!tl_lone) {
+                        tl[kTlHdr + kTlBuckets - 5] = now - tl_mt0;
+                        tl[kTlHdr + kTlBuckets - 4] = seg;
+                    }
                     tl[kTlHdr + kTlBuckets - 3] = seg;
                     tl[kTlHdr + kTlBuckets - 2] = pix;
                     tl[kTlHdr + kTlBuckets - 1] = smp;
                 }
+                tl_lone = true;
             }
         }
 #endif
@@ -1754,6 +1771,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
         const uint64_t mt_end = __builtin_amdgcn_s_memtime();
         tl_acc += (mt_end - tl_prev) * tl_busy;
         tl[kTlHdr + tl_bucket] = tl_acc;
+        for (int k = 0; k < 4; ++k) tl[kTlHdr + kTlBuckets - 9 + k] = tl_ph[k];
         tl[0] = tl_start;
         tl[1] = end;
         tl[2] = tl_dry;
