@@ -688,6 +688,17 @@ __device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const St
     T.cur = stack_pop(T, S, below);
 }
 
+// The kernel's parameters read afresh from the kernel-argument segment: a use through
+// this reference reloads the fields it needs (scalar loads, cached) instead of the
+// compiler keeping every parameter the loop touches in a scalar register across the
+// whole loop, where the product instance spilled 20 of them to vector-register lanes.
+__device__ __forceinline__ const KernelParams& kp_fresh() {
+    typedef const __attribute__((address_space(4))) KernelParams* ConstParams;
+    ConstParams q = (ConstParams)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));  // opaque: no load through q is hoisted above this point
+    return *(const KernelParams*)q;
+}
+
 // Chunks (64 work items each) a workgroup takes from the global queue per atomic.
 // One queue address serves every wave of the device and its atomics serialise
 // there: per-wave fetches left waves waiting on it (1 -> 16 chunks per atomic
@@ -1418,7 +1429,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                         // Retire the chunks no busy lane traces any more (lanes assigned in
                         // this refill have not started yet: their chunk is open regardless).
                         const bool held = L.busy || fresh_item != ~0u;
-                        acc_free = acc_retire<kAcc>(p, acc, acc_all, held, L.busy ? L.slot : fresh_slot, acc_chunk, lane);
+                        acc_free = acc_retire<kAcc>(kp_fresh(), acc, acc_all, held, L.busy ? L.slot : fresh_slot, acc_chunk,
+                                                    lane);
                     }
                     if (acc_free == 0ull) {
                         // unreachable with nothing in flight: no chunk would hold a slot
@@ -1431,7 +1443,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     ++grp_next;
                 } else {
                     uint32_t cnt = 1;
-                    c = take_chunk(p, uni, lane, grp_end >= p.late_at ? 1u : p.wave_chunks, cnt);
+                    const KernelParams& pq = kp_fresh();
+                    c = take_chunk(pq, uni, lane, grp_end >= pq.late_at ? 1u : pq.wave_chunks, cnt);
                     if (c == kPoolDone) {
                         exhausted = true;
 #ifdef TRAY_PROFILE_TIMELINE
@@ -1447,7 +1460,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 }
                 pool_next = c * 64u;
                 pool_end = pool_next + 64u;
-                pool_tile = chunk_tile(p, c);
+                const KernelParams& pc = kp_fresh();
+                pool_tile = chunk_tile(pc, c);
                 if constexpr (kAcc) {
                     // With 64 | r every item of a chunk is one pixel's: valid or padding
                     // together. A chunk of several pixel-passes (r | 64) may mix the two
@@ -1455,7 +1469,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                     int32_t cx, cj;
                     uint32_t cs, cp;
                     if (acc_rshift<kAcc>(p) < 6u ||
-                        (pool_next < p.items && decode_item(p, pool_next, pool_tile, cx, cj, cs, cp))) {
+                        (pool_next < pc.items && decode_item(pc, pool_next, pool_tile, cx, cj, cs, cp))) {
                         pool_slot = (uint32_t)__builtin_ctzll(acc_free);
                         acc_free &= ~(1ull << pool_slot);
                         acc_chunk = lane == pool_slot ? c : acc_chunk;
@@ -1487,17 +1501,18 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #endif
         if (fresh_item != ~0u) {
             TRAY_MARK("refill_cam")
+            const KernelParams& pr = kp_fresh();
             int32_t x, j;
             uint32_t smp, pass;
-            if (fresh_item < p.items && decode_item(p, fresh_item, fresh_tile, x, j, smp, pass)) {
+            if (fresh_item < pr.items && decode_item(pr, fresh_item, fresh_tile, x, j, smp, pass)) {
 #ifdef TRAY_PROBE_REFILL
                 TRAY_PROBE_F32(TRAY_PROBE_REFILL)
 #endif
                 // The pixel's primary-ray candidates, loaded before the camera ray is built.
                 uint4 cand = make_uint4(0u, 0u, 0u, kCandOverflow << 16);
                 if constexpr (kBVH)
-                    if (p.cand) cand = p.cand[(size_t)j * (size_t)p.width + (size_t)x];
-                start_sample(p, uni, L, fresh_item, x, j, (p.pass0 + pass) * (uint32_t)p.spp + smp);
+                    if (pr.cand) cand = pr.cand[(size_t)j * (size_t)pr.width + (size_t)x];
+                start_sample(pr, uni, L, fresh_item, x, j, (pr.pass0 + pass) * (uint32_t)pr.spp + smp);
                 L.slot = fresh_slot;
 #ifdef TRAY_PROFILE_REFILL
                 prof_cam = __builtin_amdgcn_s_memtime();
@@ -1554,7 +1569,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 PROF_MATERIAL(0, cam_hit);
                 bool ended = false;
                 if (cam_hit) {
-                    if (shade_step<kStats, kAcc>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
+                    if (shade_step<kStats, kAcc>(kp_fresh(), uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
                                                  [&] { return sv.bmat[max(T.slot, 0)]; }, st, acc)) {
                         ++L.segments;
                         trav_begin(T, sv, L.org, L.dir);
@@ -1710,7 +1725,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #ifdef TRAY_PROBE_SHADE64
                     TRAY_PROBE_F64(TRAY_PROBE_SHADE64)
 #endif
-                    if (shade_step<kStats, kAcc>(p, uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
+                    if (shade_step<kStats, kAcc>(kp_fresh(), uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
                                                  [&] { return sv.bmat[max(T.slot, 0)]; }, st, acc)) {
                         ++L.segments;
 #if defined(TRAY_STATS_GROUND) && !defined(TRAY_PROFILE)
