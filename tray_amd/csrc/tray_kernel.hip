@@ -149,35 +149,37 @@ __device__ __forceinline__ void disc(uint32_t wa, uint32_t wb, double radius, do
     oy = (r * s) * radius;
 }
 
-// Camera and background, copied once per workgroup into LDS and read through a
-// volatile pointer where needed: keeps ~50 dwords of loop-invariant kernel
-// arguments out of the SGPR file (they otherwise spill to VGPR lanes and cost a
-// v_readlane on every use).
+// The kernel's parameters read afresh from the kernel-argument segment: a use through
+// this reference reloads the fields it needs (scalar loads, cached) instead of the
+// compiler keeping every parameter the loop touches in a scalar register across the
+// whole loop, where the product instance spilled 20 of them to vector-register lanes.
+__device__ __forceinline__ const KernelParams& kp_fresh() {
+    typedef const __attribute__((address_space(4))) KernelParams* ConstParams;
+    ConstParams q = (ConstParams)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));  // opaque: no load through q is hoisted above this point
+    return *(const KernelParams*)q;
+}
+
+// The workgroup's chunk pool, in LDS (take_chunk). The camera, background and draw key
+// are read from the kernel arguments where they are used (callers pass kp_fresh()):
+// scalar loads at the use, neither a register held across the loop nor an LDS copy
+// re-read through vector instructions (that copy cost C2 0.7 %, C1 1.5 %, C5 0.9 %).
 struct Uniforms {
-    CamRec cam;
-    V3 bg_a, bg_b;
-    double focus_time, ray_radius;
-    uint32_t key[4];  // the draw key (rng.hpp draw_key of the seed)
     uint64_t pool;  // the workgroup's chunk pool: (end << 32) | next (take_chunk)
     uint32_t pool_chunks;  // chunks per pool refill (read only when refilling)
 };
 // Explicit LDS address space: a generic volatile pointer would be accessed with
 // (slow, system-coherent) flat loads.
 typedef const volatile __attribute__((address_space(3))) Uniforms* UniPtr;
-
-// A word of the draw key, re-read per draw and made wave-uniform (a scalar
-// operand of the hash's XORs) instead of being hoisted out of the loop, where it
-// would be spilled to a VGPR lane and cost a v_readlane on every use.
-__device__ __forceinline__ uint32_t uni_key(UniPtr uni, int i) { return __builtin_amdgcn_readfirstlane(uni->key[i]); }
-
-// The draw block of (pixel, sample, bounce, purpose) (include/tray.h, rng.hpp draw_block).
-__device__ __forceinline__ Block draw(UniPtr uni, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t purpose) {
-    return draw_block(uni_key(uni, 0), uni_key(uni, 1), uni_key(uni, 2), uni_key(uni, 3), pixel, sample, bounce,
-                      purpose);
-}
 constexpr size_t kUniformsBytes = (sizeof(Uniforms) + 255) / 256 * 256;
 
-__device__ __forceinline__ D3 ld3(const volatile __attribute__((address_space(3))) double* v) { return d3(v[0], v[1], v[2]); }
+// The draw block of (pixel, sample, bounce, purpose) (include/tray.h, rng.hpp draw_block).
+__device__ __forceinline__ Block draw(const KernelParams& p, uint32_t pixel, uint32_t sample, uint32_t bounce,
+                                     uint32_t purpose) {
+    return draw_block(p.key[0], p.key[1], p.key[2], p.key[3], pixel, sample, bounce, purpose);
+}
+
+__device__ __forceinline__ D3 ld3(const double v[3]) { return d3(v[0], v[1], v[2]); }
 
 // RandomUnitVector (ray/rand.go:30-32): Archimedes' projection of two uniforms of
 // the bounce's scatter block, z = 1 - 2 u0, r = sqrt(1 - z*z), phi = 2 pi u1.
@@ -188,32 +190,32 @@ __device__ __forceinline__ D3 unit_vector_from(double z, double r, uint32_t w1) 
 }
 
 // The sample's camera block (purpose 1): (pixel, sample, 0, 1).
-__device__ __forceinline__ Block camera_block(UniPtr uni, uint32_t pixel, uint32_t sample) {
-    return draw(uni, pixel, sample, 0u, kPurposeCamera);
+__device__ __forceinline__ Block camera_block(const KernelParams& p, uint32_t pixel, uint32_t sample) {
+    return draw(p, pixel, sample, 0u, kPurposeCamera);
 }
 
 // Camera.GetRay (ray/camera.go:113-142). The sample's camera block `u` feeds the
 // anti-aliasing disc (words 0,1; ray/tracer.go:136-139, only when r > 1) and the
 // lens disc (words 2,3, only when the aperture is open).
-__device__ __forceinline__ void get_ray(const KernelParams& p, UniPtr uni, const Block& u, double px, double py,
-                                        D3& origin, D3& dir) {
+__device__ __forceinline__ void get_ray(const KernelParams& p, const Block& u, double px, double py, D3& origin,
+                                        D3& dir) {
     double ox = 0.0, oy = 0.0;
-    const double aperture = uni->cam.aperture;
-    if (p.spp > 1) disc(u.x0, u.x1, uni->ray_radius, ox, oy);
-    const D3 pos = ld3(uni->cam.position);
-    const D3 p00 = ld3(uni->cam.pixel00);
-    const D3 pxv = ld3(uni->cam.pixel_x);
-    const D3 pyv = ld3(uni->cam.pixel_y);
+    const double aperture = p.cam.aperture;
+    if (p.spp > 1) disc(u.x0, u.x1, p.ray_radius, ox, oy);
+    const D3 pos = ld3(p.cam.position);
+    const D3 p00 = ld3(p.cam.pixel00);
+    const D3 pxv = ld3(p.cam.pixel_x);
+    const D3 pyv = ld3(p.cam.pixel_y);
     const D3 sample_pt = add(add(p00, smul(pxv, px + ox)), smul(pyv, py + oy));
     origin = pos;
     dir = sub(sample_pt, pos);
     if (aperture > 0) {
         double dx, dy;
         disc(u.x2, u.x3, 1.0, dx, dy);
-        const D3 du = ld3(uni->cam.defocus_u);
-        const D3 dv = ld3(uni->cam.defocus_v);
+        const D3 du = ld3(p.cam.defocus_u);
+        const D3 dv = ld3(p.cam.defocus_v);
         const D3 offset = add(smul(du, dx), smul(dv, dy));
-        const D3 focus_point = add(pos, smul(dir, uni->focus_time));
+        const D3 focus_point = add(pos, smul(dir, p.focus_time));
         origin = add(pos, offset);
         dir = sub(focus_point, origin);
     }
@@ -688,17 +690,6 @@ __device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const St
     T.cur = stack_pop(T, S, below);
 }
 
-// The kernel's parameters read afresh from the kernel-argument segment: a use through
-// this reference reloads the fields it needs (scalar loads, cached) instead of the
-// compiler keeping every parameter the loop touches in a scalar register across the
-// whole loop, where the product instance spilled 20 of them to vector-register lanes.
-__device__ __forceinline__ const KernelParams& kp_fresh() {
-    typedef const __attribute__((address_space(4))) KernelParams* ConstParams;
-    ConstParams q = (ConstParams)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(q));  // opaque: no load through q is hoisted above this point
-    return *(const KernelParams*)q;
-}
-
 // Chunks (64 work items each) a workgroup takes from the global queue per atomic.
 // One queue address serves every wave of the device and its atomics serialise
 // there: per-wave fetches left waves waiting on it (1 -> 16 chunks per atomic
@@ -799,7 +790,7 @@ __device__ __forceinline__ uint32_t chunk_tile(const KernelParams& p, uint32_t c
 }
 
 // Start sample s of pixel (x, compact row j) in the lane: its camera ray.
-__device__ __forceinline__ void start_sample(const KernelParams& p, UniPtr uni, Lane& L, uint32_t item, int32_t x,
+__device__ __forceinline__ void start_sample(const KernelParams& p, Lane& L, uint32_t item, int32_t x,
                                              int32_t j, uint32_t s) {
     const int32_t y = row_of(p, j);
     L.item = item;
@@ -811,7 +802,7 @@ __device__ __forceinline__ void start_sample(const KernelParams& p, UniPtr uni, 
     L.segments = 0;
     L.thr = d3(1, 1, 1);
     L.busy = true;
-    get_ray(p, uni, camera_block(uni, L.pixel, s), (double)x, (double)y, L.org, L.dir);
+    get_ray(p, camera_block(p, L.pixel, s), (double)x, (double)y, L.org, L.dir);
 }
 
 // A path ended with `color`: store it in the band's sample buffer (the resolve
@@ -977,7 +968,7 @@ __device__ __forceinline__ uint64_t acc_retire(const KernelParams& p, const AccC
 // need is done once, before them — the bounce's draw block and the unit
 // direction (sky, Metal, Dielectric).
 template <bool kStats, int kAcc, typename GeoAt, typename MatAt>
-__device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, Lane& L, int best, double closest,
+__device__ __forceinline__ bool shade_step(const KernelParams& p, Lane& L, int best, double closest,
                                            double dir_lsq, GeoAt geo_at, MatAt mat_at, Stats& st, const AccCtx& acc) {
     const bool hit = best >= 0;
     // A hit at the last level ends the path black whatever its material does
@@ -989,7 +980,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     // instead of starting after it inside the hit branch.
     const double4 g = geo_at();
     const MatRec m = mat_at();
-    const Block w = draw(uni, L.pixel, L.sample, L.bounce, kPurposeScatter);
+    const Block w = draw(p, L.pixel, L.sample, L.bounce, kPurposeScatter);
     const double u0 = uniform(w.x0);
     // Unit(r.Direction) is read by the sky, Metal and Dielectric, not by Lambertian
     // (nor a last-level hit): a wave whose shading lanes are all Lambertian hits
@@ -999,7 +990,7 @@ __device__ __forceinline__ bool shade_step(const KernelParams& p, UniPtr uni, La
     D3 color = d3(0, 0, 0);
     if (!hit) {  // AmbientLight.Hit (ray/objects.go:68-73)
         const double t = 0.5 * (ud.y + 1.0);
-        const D3 bg_a = d3(uni->bg_a.x, uni->bg_a.y, uni->bg_a.z), bg_b = d3(uni->bg_b.x, uni->bg_b.y, uni->bg_b.z);
+        const D3 bg_a = d3(p.bg_a.x, p.bg_a.y, p.bg_a.z), bg_b = d3(p.bg_b.x, p.bg_b.y, p.bg_b.z);
         color = mul(L.thr, add(smul(bg_a, 1.0 - t), smul(bg_b, t)));
     } else if (!last) {
         const D3 point = add(L.org, smul(L.dir, closest));                             // Ray.At (ray/ray.go:23-25)
@@ -1247,23 +1238,8 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     __attribute__((address_space(3))) Uniforms* uni_lds =
         (__attribute__((address_space(3))) Uniforms*)reinterpret_cast<Uniforms*>(smem_all);
     double4* smem = smem_all + kUniformsBytes / sizeof(double4);
-    if (threadIdx.x == 0) {  // scalar stores: an aggregate copy would go through scratch
+    if (threadIdx.x == 0) {
         volatile __attribute__((address_space(3))) Uniforms* u = uni_lds;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            u->cam.position[k] = p.cam.position[k];
-            u->cam.pixel00[k] = p.cam.pixel00[k];
-            u->cam.pixel_x[k] = p.cam.pixel_x[k];
-            u->cam.pixel_y[k] = p.cam.pixel_y[k];
-            u->cam.defocus_u[k] = p.cam.defocus_u[k];
-            u->cam.defocus_v[k] = p.cam.defocus_v[k];
-        }
-        u->cam.aperture = p.cam.aperture;
-        u->bg_a.x = p.bg_a.x, u->bg_a.y = p.bg_a.y, u->bg_a.z = p.bg_a.z;
-        u->bg_b.x = p.bg_b.x, u->bg_b.y = p.bg_b.y, u->bg_b.z = p.bg_b.z;
-        u->focus_time = p.focus_time;
-        u->ray_radius = p.ray_radius;
-        for (int k = 0; k < 4; ++k) u->key[k] = p.key[k];
         u->pool = 0;  // empty: the first taker refills it
         u->pool_chunks = p.pool_chunks;
     }
@@ -1332,7 +1308,6 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
     Lane L;
     L.busy = false;
     Stats st;
@@ -1479,7 +1454,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             const uint32_t n_idle = (uint32_t)__popcll(idle);
             const uint32_t take = min(n_idle, pool_end - pool_next);
             if ((idle >> lane) & 1ull) {
-                const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+                // idle lanes below this one (mbcnt: no per-lane mask held across the loop)
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 if (rank < take) {
                     fresh_item = pool_next + rank;
                     fresh_slot = pool_slot;
@@ -1512,7 +1489,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 uint4 cand = make_uint4(0u, 0u, 0u, kCandOverflow << 16);
                 if constexpr (kBVH)
                     if (pr.cand) cand = pr.cand[(size_t)j * (size_t)pr.width + (size_t)x];
-                start_sample(pr, uni, L, fresh_item, x, j, (pr.pass0 + pass) * (uint32_t)pr.spp + smp);
+                start_sample(pr, L, fresh_item, x, j, (pr.pass0 + pass) * (uint32_t)pr.spp + smp);
                 L.slot = fresh_slot;
 #ifdef TRAY_PROFILE_REFILL
                 prof_cam = __builtin_amdgcn_s_memtime();
@@ -1569,7 +1546,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 PROF_MATERIAL(0, cam_hit);
                 bool ended = false;
                 if (cam_hit) {
-                    if (shade_step<kStats, kAcc>(kp_fresh(), uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
+                    if (shade_step<kStats, kAcc>(kp_fresh(), L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
                                                  [&] { return sv.bmat[max(T.slot, 0)]; }, st, acc)) {
                         ++L.segments;
                         trav_begin(T, sv, L.org, L.dir);
@@ -1625,7 +1602,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
                 ++L.segments;
                 double closest;
                 const int best = scene_hit_linear<TRAY_UNROLL, kStats>(sv, L.org, L.dir, closest, st);
-                ended = !shade_step<kStats, kAcc>(p, uni, L, best, closest, length_sq(L.dir), [&] { return p.geo[max(best, 0)]; },  // NaN-padded: entry 0 exists
+                ended = !shade_step<kStats, kAcc>(p, L, best, closest, length_sq(L.dir), [&] { return p.geo[max(best, 0)]; },  // NaN-padded: entry 0 exists
                                                   [&] { return best >= 0 ? p.mat[best] : MatRec{}; }, st, acc);
             }
             if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
@@ -1725,7 +1702,7 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
 #ifdef TRAY_PROBE_SHADE64
                     TRAY_PROBE_F64(TRAY_PROBE_SHADE64)
 #endif
-                    if (shade_step<kStats, kAcc>(kp_fresh(), uni, L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
+                    if (shade_step<kStats, kAcc>(kp_fresh(), L, T.slot, T.closest, T.a, [&] { return sv.bgeo[max(T.slot, 0)]; },
                                                  [&] { return sv.bmat[max(T.slot, 0)]; }, st, acc)) {
                         ++L.segments;
 #if defined(TRAY_STATS_GROUND) && !defined(TRAY_PROFILE)
@@ -1751,8 +1728,9 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             }
         }
     }
-    if constexpr (kProg) flush_progress(p, prog_cur, prog_cnt, lane);
-    if constexpr (kAcc) (void)acc_retire<kAcc>(p, acc, acc_all & ~acc_free, false, 0u, acc_chunk, lane);  // every lane is idle
+    if constexpr (kProg) flush_progress(kp_fresh(), prog_cur, prog_cnt, lane);
+    if constexpr (kAcc)  // every lane is idle
+        (void)acc_retire<kAcc>(kp_fresh(), acc, acc_all & ~acc_free, false, 0u, acc_chunk, lane);
     if constexpr (kStats) {
         // One atomic per wave: 3 per lane on three addresses serialised ~9 ms of tail
         // onto every instrumented launch (786 K device-scope atomics at C2).
