@@ -38,6 +38,10 @@
  *   "work_order"          0: hand a launch's 8x8 tiles out in band order instead of
  *                         most expensive first by a counting launch's Scene.Hit
  *                         calls (same bits)
+ *   "coop_lanes"          a wave whose work queue ran dry and that holds at most
+ *                         this many paths finds their hits with the whole wave
+ *                         scanning every sphere, one path at a time (0: never;
+ *                         default 2) (same bits)
  */
 #ifndef TRAY_DEBUG_H
 #define TRAY_DEBUG_H

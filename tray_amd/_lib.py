@@ -161,7 +161,7 @@ EXPORTS = (
 DEBUG_EXPORTS = ("tray_debug_set", "tray_debug_clear")
 DEBUG_KNOBS = ("acc_slots", "band_samples", "bvh_leaf", "bvh_lds_mode", "stack_lds_slots", "node_deep",
                "primary_candidates", "resolve_staged", "wave_chunks", "scene_contexts", "grid_reserve",
-               "work_order")
+               "work_order", "coop_lanes")
 
 # tray_progress_fn: void (*)(int32_t rows, void *user)
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_void_p)

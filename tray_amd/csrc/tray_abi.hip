@@ -40,7 +40,7 @@ static std::atomic<long long> g_knob_value[kKnobCount];
 static std::atomic<bool> g_knob_set[kKnobCount];
 static const char* const kKnobNames[kKnobCount] = {
     "acc_slots", "band_samples", "bvh_leaf", "bvh_lds_mode", "stack_lds_slots", "node_deep", "primary_candidates",
-    "resolve_staged", "wave_chunks", "scene_contexts", "grid_reserve", "work_order"};
+    "resolve_staged", "wave_chunks", "scene_contexts", "grid_reserve", "work_order", "coop_lanes"};
 
 bool debug_knob(DebugKnob k, long long* v) {
     if (!g_knob_set[k].load(std::memory_order_acquire)) return false;
@@ -632,6 +632,11 @@ static int prepare_render(tray_scene_t sc, const tray_camera* cam, const tray_pa
     k.leaves = sc->leaves;
     k.leaf_single = sc->leaf_max == 1 ? 1 : 0;
     k.stack_cap = sc->stack_cap;
+    {
+        long long coop = TRAY_COOP_LANES;
+        (void)debug_knob(kKnobCoopLanes, &coop);  // A/B and tests: the drain's wave-wide Scene.Hit
+        k.coop_lanes = (uint32_t)std::max(0LL, std::min(coop, 64LL));
+    }
     // The BVH's conservative FP32 box test assumes every ray origin lies within
     // [-M, M]^3 (tray_bvh.cpp): hit points do; check the camera and lens disc.
     double cam_extent = 0;

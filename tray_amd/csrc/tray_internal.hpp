@@ -36,6 +36,7 @@ enum DebugKnob {
     kKnobSceneContexts,
     kKnobGridReserve,
     kKnobWorkOrder,
+    kKnobCoopLanes,
     kKnobCount
 };
 // True, with the value in *v, when the knob is set.

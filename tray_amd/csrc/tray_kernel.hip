@@ -690,6 +690,58 @@ __device__ __forceinline__ void trav_leaf(Trav& T, const SceneView& sv, const St
     T.cur = stack_pop(T, S, below);
 }
 
+// The drain's wave-wide Scene.Hit (KernelParams::coop_lanes; DESIGN.md 8d, "The
+// drain"). A launch ends on a few long paths, each the last of its wave: a lone
+// lane's traversal is a chain of dependent LDS reads and box tests that nothing
+// else in the wave hides (the timeline build measured 4-8 us of node steps per
+// segment of such a path, against 1.5-2 us of shading). Instead, the whole wave
+// tests every sphere of the scene for the lone ray: lane i tests slots i, i + 64,
+// ... under the any-order rule (test_geo), and the lanes' closest hits are merged
+// with the same rule (least t, then least list index). That is the reference's
+// linear scan result (ray/objects.go:37-46), which the traversal returns too: the
+// same bits, for ~8 independent sphere tests per lane at C2.
+// Scene.Hit of lane `l`'s ray (its segment's FP64 setup, T.a and T.a_inv, is done)
+// by the whole wave over `n` slots; lane l gets the hit and leaves the traversal.
+__device__ __forceinline__ void coop_hit(Trav& T, const SceneView& sv, int32_t n, const D3& org, const D3& dir,
+                                         uint32_t l, uint32_t lane) {
+    // The ray through LDS permutes, into vector registers (scalar copies would add
+    // to the loop's scalar-register pressure: round 6 measured 7 more spills, +2.1 %).
+    const int32_t src = (int32_t)l;
+    const D3 o = d3(__shfl(org.x, src, 64), __shfl(org.y, src, 64), __shfl(org.z, src, 64));
+    const D3 d = d3(__shfl(dir.x, src, 64), __shfl(dir.y, src, 64), __shfl(dir.z, src, 64));
+    Trav C;
+    C.a = __shfl(T.a, src, 64);
+    C.a_inv = __shfl(T.a_inv, src, 64);
+    C.closest = __builtin_inf();
+    C.slot = -1;
+    // Two slots per step, both loads issued before either test (like leaf_spheres).
+    for (int32_t s0 = (int32_t)lane; s0 < n; s0 += 128) {
+        const int32_t s1 = s0 + 64 < n ? s0 + 64 : s0;
+        const double4 g0 = sv.bgeo[s0], g1 = sv.bgeo[s1];
+        test_geo(C, sv, g0, s0, o, d);
+        if (s1 != s0) test_geo(C, sv, g1, s1, o, d);
+    }
+    // Merge the lanes' hits (usually a handful) in lane order, wave-uniformly.
+    uint64_t m = __ballot(C.slot >= 0);
+    double bt = __builtin_inf();
+    int32_t bs = -1;
+    while (m != 0ull) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1ull;
+        const double t = __shfl(C.closest, (int32_t)k, 64);
+        const int32_t s = __shfl(C.slot, (int32_t)k, 64);
+        bool take = t < bt;
+        if (t == bt) take = sv.bidx[s] < sv.bidx[bs];  // an exact tie: the earlier sphere of the list
+        bt = take ? t : bt;
+        bs = take ? s : bs;
+    }
+    if (lane == l) {
+        T.closest = bt;
+        T.slot = bs;
+        T.cur = kBvhNone;  // traversal done: the shade phase takes it
+    }
+}
+
 // Chunks (64 work items each) a workgroup takes from the global queue per atomic.
 // One queue address serves every wave of the device and its atomics serialise
 // there: per-wave fetches left waves waiting on it (1 -> 16 chunks per atomic
@@ -1607,6 +1659,23 @@ __global__ __launch_bounds__(kBVH ? kBvhBlock : 256, kBVH ? TRAY_BVH_WAVES_PER_S
             }
             if constexpr (kProg) count_progress(p, ended, L.j, lane, prog_cur, prog_cnt);
         } else {
+            if constexpr (kLDS == 1) {
+                // The drain: a dry wave with at most coop_lanes paths finds their hits
+                // with the whole wave (coop_hit; the node steps below then find none).
+                if (exhausted) {
+                    const KernelParams& pd = kp_fresh();
+                    if (pd.coop_lanes != 0u && (uint32_t)__popcll(__ballot(L.busy)) <= pd.coop_lanes) {
+                        PROF_T0();
+                        uint64_t m = __ballot(L.busy && T.cur != kBvhNone);
+                        while (m != 0ull) {
+                            const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                            m &= m - 1ull;
+                            coop_hit(T, sv, pd.n_slots, L.org, L.dir, l, lane);
+                        }
+                        PROF_ADD(1);
+                    }
+                }
+            }
             // Node steps for the traversing lanes.
             {
                 PROF_T0();

@@ -25,6 +25,10 @@ enum : int32_t { kOutRGBF64 = 0, kOutRGBF32 = 1, kOutRGBA8 = 2 };
 #define TRAY_BVH_BLOCK (256 * TRAY_BVH_WAVES_PER_SIMD)
 #endif
 constexpr int kBvhBlocksPerCU = 256 * TRAY_BVH_WAVES_PER_SIMD / TRAY_BVH_BLOCK;
+// KernelParams::coop_lanes unless the "coop_lanes" debug knob says otherwise.
+#ifndef TRAY_COOP_LANES
+#define TRAY_COOP_LANES 2
+#endif
 #ifdef TRAY_PROFILE
 constexpr size_t kMaxLDSBytes = (160 * 1024) / kBvhBlocksPerCU - 2048;  // diagnostic builds: 2 KB of counters
 #else
@@ -141,6 +145,10 @@ struct KernelParams {
     const uint32_t* tile_order;
     uint32_t* tile_cost;
     FastDiv div_chunks_per_tile;  // 64-item chunks per tile: rays_per_pixel x passes
+    // The drain's wave-wide Scene.Hit ("The drain"): once a wave's queue has
+    // run dry and it holds at most this many paths, each of their segments is one scan of
+    // every sphere by the whole wave instead of a one-lane traversal. 0: off.
+    uint32_t coop_lanes;
 };
 
 struct LaunchPlan;
